@@ -1,0 +1,307 @@
+/*
+ * idg_oracle.c -- CPU oracle (TEST INFRASTRUCTURE ONLY; see idg_oracle.h).
+ *
+ * Restates the reference CPU path of ska-telescope/ska-sdp-idg-bench:
+ *   gridder    app/CPU/kernels/gridder_reference.cpp:6-114
+ *   degridder  app/CPU/kernels/degridder_reference.cpp:6-129
+ *   l/m/n      app/common/math.hpp:9-24
+ *   Jones      app/common/math.hpp:26-92
+ *   metric     tests/test_util.hpp:28-92
+ *
+ * Floating-point contract.  The reference is built by GCC with
+ * `-O3 -fno-math-errno -march=native` (CMakeLists.txt:42), i.e. with FMA
+ * contraction on.  Its numbers depend on where GCC fused multiply-adds, and
+ * the repo tolerance (1e-5) is tight enough that an unfused build of the
+ * reference FAILS against the fused one.  This file is
+ * compiled with -ffp-contract=off and spells every fusion GCC made with an
+ * explicit fmaf(), so it reproduces the reference on any host compiler:
+ *   gridder   phase_index  = fma(w, n, fma(u, l, v*m))
+ *             phase_offset = fma(w_o, n, fma(u_o, l, v_o*m))
+ *             phase        = fma(-phase_index, k, phase_offset)
+ *   degridder phase_index  = fma(u, l, v*m) + w*n
+ *             phase_offset = fma(u_o, l, v_o*m) + w_o*n
+ *             phase        = fma(phase_index, k, -phase_offset)
+ *   complex a*b            = (fma(ar, br, -(ai*bi)), fma(ar, bi, ai*br))
+ *   n: tmp                 = fma(l, l, m*m)
+ * Pinned by tests/test_oracle.py against tests/golden/ (generated from the
+ * reference's own CPU path, oracle/make_golden.sh).
+ */
+#include "idg_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NCORR 4
+
+typedef struct {
+  float re, im;
+} cf;
+
+static inline cf cmul(cf a, cf b) {
+  cf r;
+  r.re = fmaf(a.re, b.re, -(a.im * b.im));
+  r.im = fmaf(a.re, b.im, a.im * b.re);
+  return r;
+}
+
+static inline cf cadd(cf a, cf b) {
+  cf r = {a.re + b.re, a.im + b.im};
+  return r;
+}
+
+/* app/common/math.hpp:9-13: evaluated in double, rounded to float. */
+static inline float lm_of(int i, int subgrid_size, float image_size) {
+  return (float)(((double)i + 0.5 - (double)(subgrid_size / 2)) *
+                 (double)image_size / (double)subgrid_size);
+}
+
+/* app/common/math.hpp:20-24 */
+static inline float n_of(float l, float m) {
+  const float tmp = fmaf(l, l, m * m);
+  return tmp > 1.0 ? 1.0f : tmp / (1.0f + sqrtf(1.0f - tmp));
+}
+
+/* 2x2 complex product c = a*b, same accumulation order as math.hpp:26-37. */
+static inline void jones_mul(const cf *a, const cf *b, cf *c) {
+  c[0] = cmul(a[0], b[0]);
+  c[1] = cmul(a[0], b[1]);
+  c[2] = cmul(a[2], b[0]);
+  c[3] = cmul(a[2], b[1]);
+  c[0] = cadd(c[0], cmul(a[1], b[2]));
+  c[1] = cadd(c[1], cmul(a[1], b[3]));
+  c[2] = cadd(c[2], cmul(a[3], b[2]));
+  c[3] = cadd(c[3], cmul(a[3], b[3]));
+}
+
+/* conjugate transpose (math.hpp:39-63) */
+static inline void jones_herm(const cf *a, cf *b) {
+  b[0].re = a[0].re; b[0].im = -a[0].im;
+  b[1].re = a[2].re; b[1].im = -a[2].im;
+  b[2].re = a[1].re; b[2].im = -a[1].im;
+  b[3].re = a[3].re; b[3].im = -a[3].im;
+}
+
+typedef struct {
+  int time_offset, nr_timesteps, aterm_index, station1, station2;
+  float u_offset, v_offset, w_offset;
+} sg_setup;
+
+/* Per-subgrid constants: gridder_reference.cpp:15-39 (identical in the
+ * degridder, degridder_reference.cpp:15-31,76-79). */
+static sg_setup setup_subgrid(const oracle_metadata *metadata, int s,
+                              int grid_size, int subgrid_size,
+                              float image_size, float w_step_in_lambda) {
+  const oracle_metadata m = metadata[s];
+  sg_setup g;
+  g.time_offset = (m.baseline_offset - metadata[0].baseline_offset) +
+                  m.time_offset;
+  g.nr_timesteps = m.nr_timesteps;
+  g.aterm_index = m.aterm_index;
+  g.station1 = (int)m.station1;
+  g.station2 = (int)m.station2;
+  const float w_offset_in_lambda =
+      (float)((double)w_step_in_lambda * ((double)m.z + 0.5));
+  const double scale = 2.0 * M_PI / (double)image_size;
+  g.u_offset = (float)((double)(m.x + subgrid_size / 2 - grid_size / 2) * scale);
+  g.v_offset = (float)((double)(m.y + subgrid_size / 2 - grid_size / 2) * scale);
+  g.w_offset = (float)(2.0 * M_PI * (double)w_offset_in_lambda);
+  return g;
+}
+
+static inline const cf *aterm_at(const float *aterms, int nr_stations,
+                                 int subgrid_size, int aterm_index,
+                                 int station, int y, int x) {
+  const size_t idx =
+      ((((size_t)aterm_index * nr_stations + station) * subgrid_size + y) *
+           subgrid_size + x) * NCORR;
+  return (const cf *)aterms + idx;
+}
+
+static void gridder_one(int s, int grid_size, int subgrid_size,
+                        float image_size, float w_step_in_lambda,
+                        int nr_channels, int nr_stations, const float *uvw,
+                        const float *wavenumbers, const cf *vis,
+                        const float *spheroidal, const float *aterms,
+                        const oracle_metadata *metadata, cf *subgrids) {
+  const int S = subgrid_size;
+  const sg_setup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                   w_step_in_lambda);
+  for (int y = 0; y < S; y++) {
+    for (int x = 0; x < S; x++) {
+      cf pix[NCORR];
+      memset(pix, 0, sizeof(pix));
+      const float l = lm_of(x, S, image_size);
+      const float m = lm_of(y, S, image_size);
+      const float n = n_of(l, m);
+      const float phase_offset =
+          fmaf(g.w_offset, n, fmaf(g.u_offset, l, g.v_offset * m));
+      for (int t = 0; t < g.nr_timesteps; t++) {
+        const size_t row = (size_t)g.time_offset + t;
+        const float u = uvw[3 * row + 0];
+        const float v = uvw[3 * row + 1];
+        const float w = uvw[3 * row + 2];
+        const float phase_index = fmaf(w, n, fmaf(u, l, v * m));
+        for (int c = 0; c < nr_channels; c++) {
+          const float phase = fmaf(-phase_index, wavenumbers[c], phase_offset);
+          cf phasor = {cosf(phase), sinf(phase)};
+          const cf *v4 = vis + (row * nr_channels + c) * NCORR;
+          for (int p = 0; p < NCORR; p++)
+            pix[p] = cadd(pix[p], cmul(v4[p], phasor));
+        }
+      }
+      /* A-term: P = A1^H * P * A2 (math.hpp:65-77) */
+      const cf *a1 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station1, y, x);
+      const cf *a2 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station2, y, x);
+      cf a1h[4], tmp[4];
+      jones_herm(a1, a1h);
+      jones_mul(a1h, pix, tmp);
+      jones_mul(tmp, a2, pix);
+      const float sph = spheroidal[y * S + x];
+      for (int p = 0; p < NCORR; p++) {
+        cf *dst = subgrids + (((size_t)s * NCORR + p) * S + y) * S + x;
+        dst->re = pix[p].re * sph;
+        dst->im = pix[p].im * sph;
+      }
+    }
+  }
+}
+
+void oracle_gridder(int nr_subgrids, int grid_size, int subgrid_size,
+                    float image_size, float w_step_in_lambda, int nr_channels,
+                    int nr_stations, const float *uvw, const float *wavenumbers,
+                    const float *visibilities, const float *spheroidal,
+                    const float *aterms, const oracle_metadata *metadata,
+                    float *subgrids, int nthreads) {
+  if (nr_subgrids <= 0) return;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+  for (int s = 0; s < nr_subgrids; s++)
+    gridder_one(s, grid_size, subgrid_size, image_size, w_step_in_lambda,
+                nr_channels, nr_stations, uvw, wavenumbers,
+                (const cf *)visibilities, spheroidal, aterms, metadata,
+                (cf *)subgrids);
+  (void)nthreads;
+}
+
+static void degridder_one(int s, int grid_size, int subgrid_size,
+                          float image_size, float w_step_in_lambda,
+                          int nr_channels, int nr_stations, const float *uvw,
+                          const float *wavenumbers, cf *vis,
+                          const float *spheroidal, const float *aterms,
+                          const oracle_metadata *metadata, const cf *subgrids,
+                          cf *pixels /* scratch [S*S*4] */) {
+  const int S = subgrid_size;
+  const sg_setup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                   w_step_in_lambda);
+  /* P' = A1 * (sph * P) * A2^H  (degridder_reference.cpp:35-74) */
+  for (int y = 0; y < S; y++) {
+    for (int x = 0; x < S; x++) {
+      const float sph = spheroidal[y * S + x];
+      cf p[4], tmp[4], a2h[4];
+      for (int c = 0; c < NCORR; c++) {
+        const cf v = subgrids[(((size_t)s * NCORR + c) * S + y) * S + x];
+        p[c].re = sph * v.re;
+        p[c].im = sph * v.im;
+      }
+      const cf *a1 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station1, y, x);
+      const cf *a2 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station2, y, x);
+      jones_mul(a1, p, tmp);
+      jones_herm(a2, a2h);
+      jones_mul(tmp, a2h, pixels + ((size_t)y * S + x) * NCORR);
+    }
+  }
+  /* degridder_reference.cpp:82-127 */
+  for (int t = 0; t < g.nr_timesteps; t++) {
+    const size_t row = (size_t)g.time_offset + t;
+    const float u = uvw[3 * row + 0];
+    const float v = uvw[3 * row + 1];
+    const float w = uvw[3 * row + 2];
+    for (int c = 0; c < nr_channels; c++) {
+      cf sum[NCORR];
+      memset(sum, 0, sizeof(sum));
+      const float k = wavenumbers[c];
+      for (int y = 0; y < S; y++) {
+        for (int x = 0; x < S; x++) {
+          const float l = lm_of(x, S, image_size);
+          const float m = lm_of(y, S, image_size);
+          const float n = n_of(l, m);
+          const float phase_index = fmaf(u, l, v * m) + w * n;
+          const float phase_offset =
+              fmaf(g.u_offset, l, g.v_offset * m) + g.w_offset * n;
+          const float phase = fmaf(phase_index, k, -phase_offset);
+          cf phasor = {cosf(phase), sinf(phase)};
+          const cf *px = pixels + ((size_t)y * S + x) * NCORR;
+          for (int p = 0; p < NCORR; p++)
+            sum[p] = cadd(sum[p], cmul(px[p], phasor));
+        }
+      }
+      cf *dst = vis + (row * nr_channels + c) * NCORR;
+      for (int p = 0; p < NCORR; p++) dst[p] = sum[p];
+    }
+  }
+}
+
+void oracle_degridder(int nr_subgrids, int grid_size, int subgrid_size,
+                      float image_size, float w_step_in_lambda,
+                      int nr_channels, int nr_stations, const float *uvw,
+                      const float *wavenumbers, float *visibilities,
+                      const float *spheroidal, const float *aterms,
+                      const oracle_metadata *metadata, const float *subgrids,
+                      int nthreads) {
+  if (nr_subgrids <= 0) return;
+  const size_t scratch = (size_t)subgrid_size * subgrid_size * NCORR;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+  {
+    cf *pixels = (cf *)malloc(scratch * sizeof(cf));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int s = 0; s < nr_subgrids; s++)
+      degridder_one(s, grid_size, subgrid_size, image_size, w_step_in_lambda,
+                    nr_channels, nr_stations, uvw, wavenumbers,
+                    (cf *)visibilities, spheroidal, aterms, metadata,
+                    (const cf *)subgrids, pixels);
+    free(pixels);
+  }
+  (void)nthreads;
+}
+
+double oracle_check_error(int64_t n, const float *A, const float *B,
+                          int64_t *nnz_out) {
+  float r_max = 1.0f, i_max = 1.0f;
+  for (int64_t i = 0; i < n; i++) {
+    const float r = fabsf(A[2 * i]), im = fabsf(A[2 * i + 1]);
+    if (r > r_max) r_max = r;
+    if (im > i_max) i_max = im;
+  }
+  double r_error = 0.0, i_error = 0.0;
+  int64_t nnz = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const float r_cmp = A[2 * i], i_cmp = A[2 * i + 1];
+    const float r_ref = B[2 * i], i_ref = B[2 * i + 1];
+    const double r_diff = (double)(r_ref - r_cmp);
+    const double i_diff = (double)(i_ref - i_cmp);
+    if (hypotf(r_ref, i_ref) > 0.0f) {
+      nnz++;
+      r_error += (r_diff * r_diff) / r_max;
+      i_error += (i_diff * i_diff) / i_max;
+    }
+  }
+  const double d = (double)(nnz > 1 ? nnz : 1);
+  if (nnz_out) *nnz_out = nnz;
+  return sqrt(r_error / d + i_error / d);
+}

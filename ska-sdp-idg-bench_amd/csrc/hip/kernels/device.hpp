@@ -1,0 +1,123 @@
+// device.hpp -- gfx950 device helpers shared by the gridder and degridder.
+//
+// Compiled with -ffp-contract=off: every fused multiply-add below is an
+// explicit __builtin_fmaf, so the phase arithmetic rounds exactly as the
+// reference build does (oracle/idg_oracle.c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "common/math.hpp"
+#include "common/types.hpp"
+
+namespace idg_mi355x {
+
+constexpr int kBlock = 256;  // 4 wave64 per workgroup
+
+// 1/(2*pi) split into a float head and tail: head + tail = 1/(2*pi) to ~2^-52.
+constexpr float kInv2PiHi = 0x1.45f306p-3f;
+constexpr float kInv2PiLo = 0x1.b9391p-28f;
+
+__device__ __forceinline__ float fma_(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+
+// Revolutions of the fp32 angle x (radians), reduced to [-0.5, 0.5] plus a
+// tail: x/(2*pi) - k with |error| <~ 3e-8 revolutions for |x| < 2^20.
+// The head product's rounding error is recovered exactly with an FMA
+// (Dekker), so no precision is lost to the ~3e3-radian phases of IDG
+// (|phase| = |phase_offset| + |phase_index * k| reaches ~525 revolutions,
+// where a plain x * (1/2pi) would be off by ~3e-5 revolutions).
+__device__ __forceinline__ float revolutions(float x) {
+  const float hi = x * kInv2PiHi;
+  float lo = fma_(x, kInv2PiHi, -hi);
+  lo = fma_(x, kInv2PiLo, lo);
+  return (hi - __builtin_rintf(hi)) + lo;
+}
+
+// sin / cos of 2*pi*r for r in revolutions.  v_sin_f32 / v_cos_f32 take
+// their argument in revolutions and are exact enough once r is small
+// (measured on MI355X: tests/probes); the range
+// reduction is done by revolutions() / the anchored update in the kernels,
+// never by the hardware's own [-256, 256] fold of a large, already-rounded
+// argument (the trap of __sinf/__cosf).
+__device__ __forceinline__ void sincos_rev(float r, float *s, float *c) {
+#if IDG_SINCOS_POLY
+  // Minimax-free fallback: quadrant split + Cody-Waite style polynomials.
+  const float q = __builtin_rintf(4.0f * r);
+  const float g = fma_(q, -0.25f, r);  // |g| <= 1/8 revolution, exact
+  const float x = g * 6.28318530717958647692f;
+  const float z = x * x;
+  float sp = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                  -1.6666654611e-1f);
+  const float sn = fma_(sp * z, x, x);
+  float cp = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                  4.166664568298827e-2f);
+  const float cs = fma_(cp * z, z, fma_(-0.5f, z, 1.0f));
+  const int qi = static_cast<int>(q) & 3;
+  const float s0 = (qi & 1) ? cs : sn;
+  const float c0 = (qi & 1) ? sn : cs;
+  *s = (qi & 2) ? -s0 : s0;
+  *c = ((qi + 1) & 2) ? -c0 : c0;
+#else
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+#endif
+}
+
+// Per-subgrid constants, evaluated exactly as the reference does
+// (gridder_reference.cpp:15-39): offsets in double, rounded to float.
+struct SubgridSetup {
+  long long time_offset;
+  int nr_timesteps, aterm_index, station1, station2;
+  float u_offset, v_offset, w_offset;
+};
+
+__device__ __forceinline__ SubgridSetup
+setup_subgrid(const idg::Metadata *__restrict__ metadata, int s,
+              int grid_size, int subgrid_size, float image_size,
+              float w_step_in_lambda) {
+  const idg::Metadata m = metadata[s];
+  const int bo0 = metadata[0].baseline_offset;
+  SubgridSetup g;
+  g.time_offset = static_cast<long long>(m.baseline_offset - bo0) +
+                  m.time_offset;
+  g.nr_timesteps = m.nr_timesteps;
+  g.aterm_index = m.aterm_index;
+  g.station1 = static_cast<int>(m.baseline.station1);
+  g.station2 = static_cast<int>(m.baseline.station2);
+  const double scale = 2.0 * 3.14159265358979323846 /
+                       static_cast<double>(image_size);
+  g.u_offset = static_cast<float>(
+      static_cast<double>(m.coordinate.x + subgrid_size / 2 - grid_size / 2) *
+      scale);
+  g.v_offset = static_cast<float>(
+      static_cast<double>(m.coordinate.y + subgrid_size / 2 - grid_size / 2) *
+      scale);
+  const float w_lambda = static_cast<float>(
+      static_cast<double>(w_step_in_lambda) *
+      (static_cast<double>(m.coordinate.z) + 0.5));
+  g.w_offset = static_cast<float>(2.0 * 3.14159265358979323846 *
+                                  static_cast<double>(w_lambda));
+  return g;
+}
+
+// Pointer to the 2x2 A-term of (slot, station, y, x).
+__device__ __forceinline__ const float4 *aterm_ptr(const float2 *aterms,
+                                                   int nr_stations, int S,
+                                                   int slot, int station,
+                                                   int y, int x) {
+  const size_t idx =
+      ((static_cast<size_t>(slot) * nr_stations + station) * S + y) * S + x;
+  return reinterpret_cast<const float4 *>(aterms + idx * 4);
+}
+
+__device__ __forceinline__ void load_jones(const float4 *p, idg::cfloat *j) {
+  const float4 a = p[0], b = p[1];
+  j[0] = {a.x, a.y};
+  j[1] = {a.z, a.w};
+  j[2] = {b.x, b.y};
+  j[3] = {b.z, b.w};
+}
+
+}  // namespace idg_mi355x

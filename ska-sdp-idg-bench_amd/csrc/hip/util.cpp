@@ -1,0 +1,421 @@
+// util.cpp -- HIP launch-and-buffer layer and MI355X runtime (see util.hpp).
+#include "util.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <memory>
+#include <sstream>
+
+#include "lib-hip.hpp"
+
+namespace hip {
+
+void hip_assert(hipError_t code, const char *file, int line, bool abort) {
+  if (code == hipSuccess) return;
+  std::fprintf(stderr, "GPUassert: %s %s %d\n", hipGetErrorString(code), file,
+               line);
+  if (abort) std::exit(static_cast<int>(code));
+}
+
+namespace {
+hipDeviceProp_t current_props() {
+  int dev = 0;
+  hipCheck(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  hipCheck(hipGetDeviceProperties(&prop, dev));
+  return prop;
+}
+}  // namespace
+
+std::string get_device_name() {
+  std::string name = current_props().name;
+  std::replace(name.begin(), name.end(), ' ', '_');
+  return name;
+}
+
+std::string extern_get_device_name() { return get_device_name(); }
+
+void print_device_info() {
+  const hipDeviceProp_t prop = current_props();
+  std::cout << "\nDevice Name " << prop.name << " (" << prop.gcnArchName
+            << ")\n"
+            << "  Memory Clock Rate (KHz): " << prop.memoryClockRate << "\n"
+            << "  Memory Bus Width (bits): " << prop.memoryBusWidth << "\n"
+            << "  Peak Memory Bandwidth (GB/s): "
+            << 2.0 * prop.memoryClockRate * (prop.memoryBusWidth / 8) / 1.0e6
+            << "\n"
+            << "  Memory size (GB): " << prop.totalGlobalMem / 1e9 << "\n"
+            << "  Compute Units: " << prop.multiProcessorCount << "\n"
+            << std::endl;
+}
+
+std::vector<int> get_launch_kernel_dimensions() {
+  const hipDeviceProp_t prop = current_props();
+  return {prop.multiProcessorCount, prop.maxThreadsPerBlock};
+}
+
+int get_cu_nr() { return current_props().multiProcessorCount; }
+int get_max_threads() { return current_props().maxThreadsPerBlock; }
+size_t get_gmem_size() { return current_props().totalGlobalMem; }
+int get_cu_freq() { return current_props().clockRate; }
+
+void print_dimensions(dim3 g, dim3 b) {
+  std::cout << "Dimensions: (" << g.x << "," << g.y << "," << g.z << ") - ("
+            << b.x << "," << b.y << "," << b.z << ")\n"
+            << std::endl;
+}
+
+double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
+                    void **args, std::string func_name, double gflops,
+                    double gbytes, double mvis) {
+  const int warm = static_cast<int>(get_env_var("NR_WARM_UP_RUNS", 2));
+  const int iters =
+      std::max(1, static_cast<int>(get_env_var("NR_ITERATIONS", 5)));
+  hipEvent_t start, stop;
+  hipCheck(hipEventCreate(&start));
+  hipCheck(hipEventCreate(&stop));
+  for (int i = 0; i < warm; ++i)
+    hipCheck(hipLaunchKernel(func, gridDim, blockDim, args, 0, nullptr));
+  hipCheck(hipDeviceSynchronize());
+  hipCheck(hipEventRecord(start, nullptr));
+  for (int i = 0; i < iters; ++i)
+    hipCheck(hipLaunchKernel(func, gridDim, blockDim, args, 0, nullptr));
+  hipCheck(hipEventRecord(stop, nullptr));
+  hipCheck(hipEventSynchronize(stop));
+  float ms = 0.0f;
+  hipCheck(hipEventElapsedTime(&ms, start, stop));
+  hipCheck(hipEventDestroy(start));
+  hipCheck(hipEventDestroy(stop));
+  const double seconds = 1e-3 * ms / iters;
+  report(func_name, seconds, gflops, gbytes, mvis);
+  report_csv(func_name, get_device_name(), "-hip.csv", seconds, gflops, gbytes,
+             mvis);
+  return seconds;
+}
+
+void c_run_kernel(const void *func, dim3 gridDim, dim3 blockDim, void **args) {
+  hipCheck(hipLaunchKernel(func, gridDim, blockDim, args, 0, nullptr));
+}
+
+void p_run_gridder_(const void *func, std::string func_name, int num_threads) {
+  idg_mi355x::run_performance(idg_mi355x::Direction::kGridder, func,
+                              func_name, num_threads);
+}
+
+void p_run_degridder_(const void *func, std::string func_name,
+                      int num_threads) {
+  idg_mi355x::run_performance(idg_mi355x::Direction::kDegridder, func,
+                              func_name, num_threads);
+}
+
+namespace {
+// Shared body of c_run_gridder_ / c_run_degridder_: the reference semantics
+// (allocate, copy in, one launch, copy out, free) with validation.
+void c_run_common(idg_mi355x::Direction dir, int nr_subgrids, int grid_size,
+                  int subgrid_size, float image_size, float w_step_in_lambda,
+                  int nr_channels, int nr_stations,
+                  idg::Array2D<idg::UVWCoordinate<float>> &uvw,
+                  idg::Array1D<float> &wavenumbers,
+                  idg::Array3D<idg::Visibility<std::complex<float>>> &vis,
+                  idg::Array2D<float> &spheroidal,
+                  idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
+                  idg::Array1D<idg::Metadata> &metadata,
+                  idg::Array4D<std::complex<float>> &subgrids,
+                  const void *func, int num_threads) {
+  idg_mi355x::Problem p;
+  p.nr_subgrids = nr_subgrids;
+  p.grid_size = grid_size;
+  p.subgrid_size = subgrid_size;
+  p.image_size = image_size;
+  p.w_step_in_lambda = w_step_in_lambda;
+  p.nr_channels = nr_channels;
+  p.nr_stations = nr_stations;
+  idg_mi355x::Extents e;
+  e.uvw_rows = uvw.size();
+  e.aterm_slots = aterms.get_w_dim();
+  std::string msg;
+  idg_mi355x::KernelChoice force;
+  force.func = func;
+  force.name = "caller-supplied";
+  force.block = num_threads;
+  const hipError_t err = idg_mi355x::run_host(
+      dir, p, e, uvw.data(), wavenumbers.data(), vis.data(),
+      spheroidal.data(), aterms.data(), metadata.data(), subgrids.data(),
+      &msg, func ? &force : nullptr);
+  if (!msg.empty()) {
+    std::fprintf(stderr, "idg-mi355x: %s\n", msg.c_str());
+    std::exit(EXIT_FAILURE);
+  }
+  hipCheck(err);
+}
+}  // namespace
+
+// The func/num_threads arguments of the reference signature are honoured:
+// a kernel with the 13-argument ABI is launched with grid = nr_subgrids,
+// block = num_threads; func == nullptr selects the MI355X kernel.
+void c_run_gridder_(
+    int nr_subgrids, int grid_size, int subgrid_size, float image_size,
+    float w_step_in_lambda, int nr_channels, int nr_stations,
+    idg::Array2D<idg::UVWCoordinate<float>> &uvw,
+    idg::Array1D<float> &wavenumbers,
+    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities,
+    idg::Array2D<float> &spheroidal,
+    idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
+    idg::Array1D<idg::Metadata> &metadata,
+    idg::Array4D<std::complex<float>> &subgrids, const void *func,
+    int num_threads) {
+  c_run_common(idg_mi355x::Direction::kGridder, nr_subgrids, grid_size,
+               subgrid_size, image_size, w_step_in_lambda, nr_channels,
+               nr_stations, uvw, wavenumbers, visibilities, spheroidal, aterms,
+               metadata, subgrids, func, num_threads);
+}
+
+void c_run_degridder_(
+    int nr_subgrids, int grid_size, int subgrid_size, float image_size,
+    float w_step_in_lambda, int nr_channels, int nr_stations,
+    idg::Array2D<idg::UVWCoordinate<float>> &uvw,
+    idg::Array1D<float> &wavenumbers,
+    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities,
+    idg::Array2D<float> &spheroidal,
+    idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
+    idg::Array1D<idg::Metadata> &metadata,
+    idg::Array4D<std::complex<float>> &subgrids, const void *func,
+    int num_threads) {
+  c_run_common(idg_mi355x::Direction::kDegridder, nr_subgrids, grid_size,
+               subgrid_size, image_size, w_step_in_lambda, nr_channels,
+               nr_stations, uvw, wavenumbers, visibilities, spheroidal, aterms,
+               metadata, subgrids, func, num_threads);
+}
+
+void print_benchmark() {
+  std::cout << ">>> hip IDG BENCHMARK (MI355X / gfx950)" << std::endl;
+}
+
+}  // namespace hip
+
+namespace idg_mi355x {
+
+std::string validate(const Problem &p, const Extents &e,
+                     const idg::Metadata *md) {
+  std::ostringstream err;
+  if (p.nr_subgrids < 0) return "nr_subgrids < 0";
+  if (p.nr_subgrids == 0) return "";
+  if (p.subgrid_size <= 0) return "subgrid_size must be > 0";
+  if (p.nr_channels <= 0) return "nr_channels must be > 0";
+  if (p.nr_stations <= 0) return "nr_stations must be > 0";
+  if (md == nullptr) return "metadata is null";
+  const long long bo0 = md[0].baseline_offset;
+  for (int s = 0; s < p.nr_subgrids; ++s) {
+    const idg::Metadata &m = md[s];
+    const long long t0 = (m.baseline_offset - bo0) + (long long)m.time_offset;
+    if (m.nr_timesteps < 0 || t0 < 0 ||
+        t0 + m.nr_timesteps > static_cast<long long>(e.uvw_rows)) {
+      err << "subgrid " << s << ": timesteps [" << t0 << ", "
+          << t0 + m.nr_timesteps << ") outside uvw/visibility rows [0, "
+          << e.uvw_rows << ")";
+      return err.str();
+    }
+    if (m.aterm_index < 0 ||
+        static_cast<size_t>(m.aterm_index) >= e.aterm_slots) {
+      err << "subgrid " << s << ": aterm_index " << m.aterm_index
+          << " outside [0, " << e.aterm_slots << ")";
+      return err.str();
+    }
+    if (m.baseline.station1 >= static_cast<unsigned>(p.nr_stations) ||
+        m.baseline.station2 >= static_cast<unsigned>(p.nr_stations)) {
+      err << "subgrid " << s << ": station (" << m.baseline.station1 << ","
+          << m.baseline.station2 << ") outside [0, " << p.nr_stations << ")";
+      return err.str();
+    }
+  }
+  return "";
+}
+
+hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
+                  const float *d_wavenumbers, void *d_visibilities,
+                  const float *d_spheroidal, const void *d_aterms,
+                  const void *d_metadata, void *d_subgrids,
+                  hipStream_t stream, const KernelChoice *force) {
+  if (p.nr_subgrids <= 0) return hipSuccess;
+  const KernelChoice k =
+      force ? *force
+            : (dir == Direction::kGridder ? select_gridder(p)
+                                          : select_degridder(p));
+  if (k.func == nullptr) return hipErrorInvalidConfiguration;
+  int grid_size = p.grid_size, subgrid_size = p.subgrid_size;
+  float image_size = p.image_size, w_step = p.w_step_in_lambda;
+  int nr_channels = p.nr_channels, nr_stations = p.nr_stations;
+  void *args[] = {&grid_size,     &subgrid_size,    &image_size,
+                  &w_step,        &nr_channels,     &nr_stations,
+                  &d_uvw,         &d_wavenumbers,   &d_visibilities,
+                  &d_spheroidal,  &d_aterms,        &d_metadata,
+                  &d_subgrids};
+  return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args, 0,
+                         stream);
+}
+
+namespace {
+// RAII device buffer.
+struct DevBuf {
+  void *ptr = nullptr;
+  hipError_t alloc(size_t bytes) {
+    return bytes ? hipMalloc(&ptr, bytes) : hipSuccess;
+  }
+  ~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+};
+#define IDG_TRY(x)                   \
+  do {                               \
+    hipError_t e_ = (x);             \
+    if (e_ != hipSuccess) return e_; \
+  } while (0)
+}  // namespace
+
+hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
+                    const void *uvw, const float *wavenumbers,
+                    void *visibilities, const float *spheroidal,
+                    const void *aterms, const idg::Metadata *metadata,
+                    void *subgrids, std::string *msg,
+                    const KernelChoice *force) {
+  const std::string bad = validate(p, e, metadata);
+  if (!bad.empty()) {
+    if (msg) *msg = bad;
+    return hipErrorInvalidValue;
+  }
+  if (p.nr_subgrids == 0) return hipSuccess;
+  const size_t S = static_cast<size_t>(p.subgrid_size);
+  const size_t b_uvw = e.uvw_rows * 3 * sizeof(float);
+  const size_t b_wn = static_cast<size_t>(p.nr_channels) * sizeof(float);
+  const size_t b_vis = e.uvw_rows * p.nr_channels * 4 * 2 * sizeof(float);
+  const size_t b_sph = S * S * sizeof(float);
+  const size_t b_at = e.aterm_slots * p.nr_stations * S * S * 4 * 2 *
+                      sizeof(float);
+  const size_t b_md = static_cast<size_t>(p.nr_subgrids) * sizeof(idg::Metadata);
+  const size_t b_sg = static_cast<size_t>(p.nr_subgrids) * 4 * S * S * 2 *
+                      sizeof(float);
+  DevBuf d_uvw, d_wn, d_vis, d_sph, d_at, d_md, d_sg;
+  IDG_TRY(d_uvw.alloc(b_uvw));
+  IDG_TRY(d_wn.alloc(b_wn));
+  IDG_TRY(d_vis.alloc(b_vis));
+  IDG_TRY(d_sph.alloc(b_sph));
+  IDG_TRY(d_at.alloc(b_at));
+  IDG_TRY(d_md.alloc(b_md));
+  IDG_TRY(d_sg.alloc(b_sg));
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  IDG_TRY(hipMemcpy(d_uvw.ptr, uvw, b_uvw, h2d));
+  IDG_TRY(hipMemcpy(d_wn.ptr, wavenumbers, b_wn, h2d));
+  IDG_TRY(hipMemcpy(d_sph.ptr, spheroidal, b_sph, h2d));
+  IDG_TRY(hipMemcpy(d_at.ptr, aterms, b_at, h2d));
+  IDG_TRY(hipMemcpy(d_md.ptr, metadata, b_md, h2d));
+  if (dir == Direction::kGridder)
+    IDG_TRY(hipMemcpy(d_vis.ptr, visibilities, b_vis, h2d));
+  else
+    IDG_TRY(hipMemcpy(d_sg.ptr, subgrids, b_sg, h2d));
+  IDG_TRY(launch(dir, p, d_uvw.ptr, static_cast<const float *>(d_wn.ptr),
+                 d_vis.ptr, static_cast<const float *>(d_sph.ptr), d_at.ptr,
+                 d_md.ptr, d_sg.ptr, nullptr, force));
+  IDG_TRY(hipGetLastError());
+  if (dir == Direction::kGridder)
+    IDG_TRY(hipMemcpy(subgrids, d_sg.ptr, b_sg, hipMemcpyDeviceToHost));
+  else
+    IDG_TRY(hipMemcpy(visibilities, d_vis.ptr, b_vis, hipMemcpyDeviceToHost));
+  return hipDeviceSynchronize();
+}
+
+double run_performance(Direction dir, const void *func, std::string name,
+                       int num_threads) {
+  const int nr_correlations =
+      static_cast<int>(get_env_var("NR_CORRELATIONS", 4));
+  const int grid_size = static_cast<int>(get_env_var("GRID_SIZE", 1024));
+  const int subgrid_size = static_cast<int>(get_env_var("SUBGRID_SIZE", 32));
+  const int nr_stations = static_cast<int>(get_env_var("NR_STATIONS", 50));
+  const int nr_timeslots = static_cast<int>(get_env_var("NR_TIMESLOTS", 20));
+  const int nr_timesteps =
+      static_cast<int>(get_env_var("NR_TIMESTEPS_SUBGRID", 128));
+  const int nr_channels = static_cast<int>(get_env_var("NR_CHANNELS", 16));
+  const int nr_baselines = nr_stations * (nr_stations - 1) / 2;
+  const int nr_subgrids = nr_baselines * nr_timeslots;
+  const size_t rows = static_cast<size_t>(nr_subgrids) * nr_timesteps;
+  if (nr_correlations != 4)
+    std::cerr << "idg-mi355x: kernels compute 4 correlations; "
+                 "NR_CORRELATIONS only affects the work model\n";
+  print_parameters(nr_stations, nr_channels, nr_timesteps, nr_correlations,
+                   nr_timeslots, IMAGE_SIZE, grid_size, subgrid_size, W_STEP,
+                   nr_baselines, nr_subgrids, static_cast<int>(rows));
+  const double gflops =
+      1e-9 * flops_gridder(nr_channels, rows, nr_subgrids, subgrid_size,
+                           nr_correlations);
+  const double gbytes =
+      1e-9 * bytes_gridder(nr_channels, rows, nr_subgrids, subgrid_size,
+                           nr_correlations);
+  const double mvis = 1e-6 * rows * nr_channels;
+
+  // Real synthetic inputs (documented deviation from the reference, which
+  // uploads only the metadata).
+  srand(0);
+  idg::Array2D<idg::UVWCoordinate<float>> uvw(nr_subgrids, nr_timesteps);
+  idg::Array1D<float> freq(nr_channels), wn(nr_channels);
+  idg::Array1D<idg::Baseline> baselines(nr_baselines);
+  idg::Array2D<float> sph(subgrid_size, subgrid_size);
+  idg::Array4D<idg::Matrix2x2<std::complex<float>>> aterms(
+      nr_timeslots, nr_stations, subgrid_size, subgrid_size);
+  idg::Array1D<idg::Metadata> md(nr_subgrids);
+  initialize_uvw(grid_size, uvw);
+  initialize_frequencies(freq);
+  initialize_wavenumbers(freq, wn);
+  initialize_baselines(nr_stations, baselines);
+  initialize_spheroidal(sph);
+  initialize_aterms(sph, aterms);
+  initialize_metadata(grid_size, nr_timeslots, nr_timesteps, baselines, md);
+  idg::Array3D<idg::Visibility<std::complex<float>>> vis(nr_subgrids,
+                                                         nr_timesteps,
+                                                         nr_channels);
+  idg::Array4D<std::complex<float>> subgrids(nr_subgrids, 4, subgrid_size,
+                                             subgrid_size);
+  if (dir == Direction::kGridder)
+    initialize_visibilities(grid_size, IMAGE_SIZE, freq, uvw, vis);
+  else
+    initialize_subgrids(subgrids);
+
+  Problem p{nr_subgrids, grid_size, subgrid_size, IMAGE_SIZE,
+            static_cast<float>(W_STEP), nr_channels, nr_stations};
+  Extents e{rows, static_cast<size_t>(nr_timeslots)};
+  const std::string bad = validate(p, e, md.data());
+  if (!bad.empty()) {
+    std::cerr << "idg-mi355x: " << bad << std::endl;
+    std::exit(EXIT_FAILURE);
+  }
+  void *d_uvw, *d_wn, *d_vis, *d_sph, *d_at, *d_md, *d_sg;
+  hipCheck(hipMalloc(&d_uvw, uvw.bytes()));
+  hipCheck(hipMalloc(&d_wn, wn.bytes()));
+  hipCheck(hipMalloc(&d_vis, vis.bytes()));
+  hipCheck(hipMalloc(&d_sph, sph.bytes()));
+  hipCheck(hipMalloc(&d_at, aterms.bytes()));
+  hipCheck(hipMalloc(&d_md, md.bytes()));
+  hipCheck(hipMalloc(&d_sg, subgrids.bytes()));
+  hipCheck(hipMemcpy(d_uvw, uvw.data(), uvw.bytes(), hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_wn, wn.data(), wn.bytes(), hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_vis, vis.data(), vis.bytes(), hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_sph, sph.data(), sph.bytes(), hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_at, aterms.data(), aterms.bytes(),
+                     hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_md, md.data(), md.bytes(), hipMemcpyHostToDevice));
+  hipCheck(hipMemcpy(d_sg, subgrids.data(), subgrids.bytes(),
+                     hipMemcpyHostToDevice));
+  int a_grid = grid_size, a_sub = subgrid_size, a_nc = nr_channels,
+      a_ns = nr_stations;
+  float a_img = IMAGE_SIZE, a_w = W_STEP;
+  void *args[] = {&a_grid, &a_sub, &a_img, &a_w,   &a_nc,  &a_ns, &d_uvw,
+                  &d_wn,   &d_vis, &d_sph, &d_at,  &d_md,  &d_sg};
+  const double seconds =
+      hip::p_run_kernel(func, dim3(nr_subgrids), dim3(num_threads), args, name,
+                        gflops, gbytes, mvis);
+  for (void *ptr : {d_uvw, d_wn, d_vis, d_sph, d_at, d_md, d_sg})
+    hipCheck(hipFree(ptr));
+  return seconds;
+}
+
+}  // namespace idg_mi355x

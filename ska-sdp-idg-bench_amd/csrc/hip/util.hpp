@@ -1,0 +1,147 @@
+// util.hpp -- the HIP launch-and-buffer layer.
+//
+// Keeps the reference's app/HIP/util.hpp:13-63 API (p_run_kernel,
+// c_run_kernel, p_run_gridder_ / c_run_gridder_, p_run_degridder_ /
+// c_run_degridder_, device queries) so a kernel TU written against the
+// reference drops in here and vice versa.  Differences, all deliberate:
+//   * sizes are size_t end to end (the reference's int products overflow at
+//     nr_channels = 256, util.cpp:220-231);
+//   * every HIP call is checked; metadata is validated against the buffer
+//     sizes on the host before any launch (a bad index would fault the GPU);
+//   * the perf entry uploads real synthetic inputs (the reference times
+//     kernels on uninitialised memory, util.cpp:234-235);
+//   * launches go to an explicit stream (nullptr = legacy default stream).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "lib-common.hpp"
+
+namespace hip {
+
+// Aborts the process on error, as the reference's hipCheck does
+// (util.cpp:5-15).
+#define hipCheck(ans) ::hip::hip_assert((ans), __FILE__, __LINE__)
+void hip_assert(hipError_t code, const char *file, int line, bool abort = true);
+
+std::string get_device_name();
+void print_device_info();
+std::vector<int> get_launch_kernel_dimensions();
+int get_cu_nr();
+int get_max_threads();
+size_t get_gmem_size();
+int get_cu_freq();
+void print_dimensions(dim3 gridDim, dim3 blockDim);
+
+// Warm-up + event-timed loop of NR_ITERATIONS launches, then report() and
+// report_csv() (reference util.cpp:81-165).  Returns seconds per launch.
+double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
+                    void **args, std::string func_name = "",
+                    double gflops = 0, double gbytes = 0, double mvis = 0);
+
+// One launch (reference util.cpp:167-174).
+void c_run_kernel(const void *func, dim3 gridDim, dim3 blockDim, void **args);
+
+void p_run_gridder_(const void *func, std::string func_name, int num_threads);
+
+void c_run_gridder_(
+    int nr_subgrids, int grid_size, int subgrid_size, float image_size,
+    float w_step_in_lambda, int nr_channels, int nr_stations,
+    idg::Array2D<idg::UVWCoordinate<float>> &uvw,
+    idg::Array1D<float> &wavenumbers,
+    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities,
+    idg::Array2D<float> &spheroidal,
+    idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
+    idg::Array1D<idg::Metadata> &metadata,
+    idg::Array4D<std::complex<float>> &subgrids, const void *func,
+    int num_threads);
+
+void p_run_degridder_(const void *func, std::string func_name,
+                      int num_threads);
+
+void c_run_degridder_(
+    int nr_subgrids, int grid_size, int subgrid_size, float image_size,
+    float w_step_in_lambda, int nr_channels, int nr_stations,
+    idg::Array2D<idg::UVWCoordinate<float>> &uvw,
+    idg::Array1D<float> &wavenumbers,
+    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities,
+    idg::Array2D<float> &spheroidal,
+    idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
+    idg::Array1D<idg::Metadata> &metadata,
+    idg::Array4D<std::complex<float>> &subgrids, const void *func,
+    int num_threads);
+
+void print_benchmark();
+
+}  // namespace hip
+
+// ---------------------------------------------------------------------------
+// MI355X runtime: kernel selection, validation and raw-pointer pipelines.
+// Used by the kernel TUs, by util.cpp and by the C ABI (capi/idg_capi.cpp).
+// ---------------------------------------------------------------------------
+namespace idg_mi355x {
+
+enum class Direction { kGridder = 0, kDegridder = 1 };
+
+// Geometry of one gridder/degridder call; the 13-argument kernel ABI of the
+// reference carries the same values.
+struct Problem {
+  int nr_subgrids = 0;
+  int grid_size = 0;
+  int subgrid_size = 0;
+  float image_size = IMAGE_SIZE;
+  float w_step_in_lambda = W_STEP;
+  int nr_channels = 0;
+  int nr_stations = 0;
+};
+
+// Buffer extents used for host-side validation (element counts).
+struct Extents {
+  size_t uvw_rows = 0;      // UVW triplets (= visibility rows)
+  size_t aterm_slots = 0;   // leading dimension of aterms (timeslots)
+};
+
+struct KernelChoice {
+  const void *func = nullptr;  // __global__ with the 13-argument ABI
+  const char *name = "";
+  int block = 256;
+  int grid = 0;  // = nr_subgrids
+};
+
+// Defined in the kernel TUs.
+KernelChoice select_gridder(const Problem &p);
+KernelChoice select_degridder(const Problem &p);
+
+// Returns an empty string if every subgrid's time range, stations and A-term
+// slot lie inside the buffers, else a description of the first violation.
+std::string validate(const Problem &p, const Extents &e,
+                     const idg::Metadata *metadata);
+
+// Asynchronous launch on device buffers (the C-ABI idg_*_launch path).
+// `force` launches a caller-supplied 13-argument kernel instead of the
+// selected one (the func/num_threads arguments of c_run_gridder_).
+hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
+                  const float *d_wavenumbers, void *d_visibilities,
+                  const float *d_spheroidal, const void *d_aterms,
+                  const void *d_metadata, void *d_subgrids,
+                  hipStream_t stream, const KernelChoice *force = nullptr);
+
+// Synchronous host-buffer pipeline: validate, allocate, H2D, launch, D2H,
+// free.  Returns hipSuccess or the first error; *msg explains validation
+// failures.
+hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
+                    const void *uvw, const float *wavenumbers,
+                    void *visibilities, const float *spheroidal,
+                    const void *aterms, const idg::Metadata *metadata,
+                    void *subgrids, std::string *msg,
+                    const KernelChoice *force = nullptr);
+
+// Perf entry shared by p_run_gridder_/p_run_degridder_: env-configured
+// problem, synthetic inputs, timed launches.  Returns seconds per launch.
+double run_performance(Direction dir, const void *func, std::string name,
+                       int num_threads);
+
+}  // namespace idg_mi355x
