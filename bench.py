@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench.py -- IDG gridder + degridder throughput on MI355X (BASELINE.json metric).
+
+One step = one gridder pass + one degridder pass over one batch of the
+workload, both kernels on the same HIP stream, inputs resident in HBM.  At
+N=1 the batch is BASELINE.json configs[1], the reference's perf defaults
+(app/HIP/util.cpp:181-187): NR_STATIONS=50, NR_TIMESLOTS=20,
+NR_TIMESTEPS_SUBGRID=128, NR_CHANNELS=16, SUBGRID_SIZE=32, GRID_SIZE=1024
+-> 24,500 subgrids, 50.176 M visibilities, with the reference's own synthetic
+generators (srand(0)).  With N GPUs (one process per GPU, torchrun) every
+rank processes its own batch of that size -- weak scaling, subgrid-sharded,
+no collective on the data path; value = all ranks' visibilities / the max
+over ranks of the timed region.
+
+`value` counts a visibility once per step (it is gridded AND degridded);
+per-kernel Mvis/s are reported alongside.  The roofline object is for the
+dominant (slower) kernel: achieved = the reference work model's FLOPs per
+launch (app/common/common.cpp:100-129; 35,459 FLOP/vis at this config) /
+that kernel's mean duration from HIP events on its stream; peak = MI355X FP32
+(157.3 TFLOP/s -- vector and f32-MFMA peaks are equal on gfx950).  The path is
+compute-bound; its HBM roofline fraction is reported too.  cpu_baseline times
+the reference's own CPU path (oracle/_ref, 1 thread, as the reference builds
+it) on a bounded sample of the same batch.
+
+    python bench.py [--gpus N --steps K --warmup W] [--workload default]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ska-sdp-idg-bench_amd"))
+
+METRIC = "Mvisibilities/s (gridder & degridder) at 1/2/4/8 GPUs; % HBM roofline"
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # BASELINE.json configs[1] (the metric's config)
+    "default": dict(nr_stations=50, nr_timeslots=20, nr_timesteps=128,
+                    nr_channels=16, grid_size=1024, subgrid_size=32),
+    # configs[2]: large channel count (25.7 GB of visibilities per batch)
+    "c256": dict(nr_stations=50, nr_timeslots=20, nr_timesteps=128,
+                 nr_channels=256, grid_size=1024, subgrid_size=32),
+    # configs[4]: large subgrid, A-term + spheroidal
+    "s64": dict(nr_stations=50, nr_timeslots=20, nr_timesteps=128,
+                nr_channels=16, grid_size=1024, subgrid_size=64),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="default", choices=sorted(WORKLOADS))
+    ap.add_argument("--timeslots", type=int, default=None,
+                    help="override NR_TIMESLOTS (batch size)")
+    ap.add_argument("--cpu-sample-subgrids", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(
+        REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(w, a, nsample):
+    """Time the reference CPU path (oracle/_ref, else the oracle port) on the
+    first `nsample` subgrids of the batch.  Test infrastructure only: the
+    baseline the GPU number is reported beside, never the measured path."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+    n = min(nsample, a["metadata"].size)
+    md = a["metadata"][:n]
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+    args = (n, w["grid_size"], S, 0.01, 0.0, C, w["nr_stations"])
+    if orc.Reference.available(portable=True):
+        impl, kind = orc.Reference(portable=True), "reference"
+        extra = {}
+    else:
+        impl, kind = orc.Oracle(), "port"
+        extra = {"nthreads": 1}
+    sg = np.zeros((n, 4, S, S, 2), np.float32)
+    t0 = time.perf_counter()
+    impl.gridder(*args, a["uvw"], a["wavenumbers"], a["visibilities"],
+                 a["spheroidal"], a["aterms"], md, sg, **extra)
+    t1 = time.perf_counter()
+    vis = np.zeros((n, T, C, 4, 2), np.float32)
+    impl.degridder(*args, a["uvw"], a["wavenumbers"], vis, a["spheroidal"],
+                   a["aterms"], md, np.ascontiguousarray(a["subgrids"][:n]),
+                   **extra)
+    t2 = time.perf_counter()
+    nvis = n * T * C
+    return {
+        "value": round(nvis / (t2 - t0) / 1e6, 4),
+        "unit": "Mvis/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": (f"first {n} subgrids of the same batch ({nvis} vis), "
+                   f"gridder {t1 - t0:.2f} s + degridder {t2 - t1:.2f} s, "
+                   f"{'oracle/_ref/libidgref_v3.so (reference app/CPU)' if kind == 'reference' else 'oracle/liboracle.so'}"
+                   ", single thread as the reference builds it"),
+        "gridder_mvis_s": round(nvis / (t1 - t0) / 1e6, 4),
+        "degridder_mvis_s": round(nvis / (t2 - t1) / 1e6, 4),
+    }
+
+
+def traffic_for(path, workload, kernel):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t[workload][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import idg_amd
+    from idg_amd import dist
+
+    rank, local_rank, world = dist.init()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    w = dict(WORKLOADS[args.workload])
+    if args.timeslots:
+        w["nr_timeslots"] = args.timeslots
+    st, ts, T, C, G, S = (w["nr_stations"], w["nr_timeslots"],
+                          w["nr_timesteps"], w["nr_channels"], w["grid_size"],
+                          w["subgrid_size"])
+    ns = idg_amd.nr_subgrids_for(st, ts)
+    nvis = ns * T * C
+
+    # ---- synthetic batch (reference generators), resident in HBM ----------
+    threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    a = idg_amd.generate(st, ts, T, C, G, S, nthreads=threads)
+    idg_amd.validate_metadata(ns, S, C, st, ns * T, ts, a["metadata"])
+    dev = {k: torch.from_numpy(a[k]).cuda() for k in
+           ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms",
+            "subgrids")}
+    dev["metadata"] = torch.from_numpy(
+        a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
+    grid_out = torch.empty_like(dev["subgrids"])
+    degrid_out = torch.empty_like(dev["visibilities"])
+    p = (ns, G, S, idg_amd.IMAGE_SIZE, idg_amd.W_STEP, C, st)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        idg_amd.gridder_launch(*p, dev["uvw"], dev["wavenumbers"],
+                               dev["visibilities"], dev["spheroidal"],
+                               dev["aterms"], dev["metadata"], grid_out,
+                               stream=stream)
+        if ev:
+            ev[1].record(stream)
+        idg_amd.degridder_launch(*p, dev["uvw"], dev["wavenumbers"],
+                                 degrid_out, dev["spheroidal"], dev["aterms"],
+                                 dev["metadata"], dev["subgrids"],
+                                 stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for _ in range(args.steps)]
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = dist.max_over_ranks(elapsed)
+
+    t_grid = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3
+    t_degrid = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps / 1e3
+    t_grid = dist.max_over_ranks(t_grid)
+    t_degrid = dist.max_over_ranks(t_degrid)
+    sec_per_step = elapsed_max / args.steps
+
+    flops = idg_amd.flops_gridder(C, ns * T, ns, S)
+    nbytes = idg_amd.bytes_gridder(C, ns * T, ns, S)
+    kernels = {}
+    for name, t in (("gridder", t_grid), ("degridder", t_degrid)):
+        kname = idg_amd.kernel_name(name, S, C)
+        kernels[name] = {
+            "kernel": kname,
+            "ms": round(t * 1e3, 4),
+            "mvis_s_per_gpu": round(nvis / t / 1e6, 2),
+            "tflops": round(flops / t / 1e12, 3),
+            "fp32_frac": round(flops / t / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "hbm_gbs_model": round(nbytes / t / 1e9, 2),
+        }
+    dom = "gridder" if t_grid >= t_degrid else "degridder"
+    t_dom = t_grid if dom == "gridder" else t_degrid
+    achieved = flops / t_dom / 1e12
+    roofline = {
+        "bound": "mfma",
+        "achieved": round(achieved, 3),
+        "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+        "traffic": traffic_for(args.traffic_file, args.workload,
+                               kernels[dom]["kernel"]),
+        "kernel": kernels[dom]["kernel"],
+        "note": ("FP32-compute-bound (VALU FMA + v_sin/v_cos; gfx950 FP32 "
+                 "vector peak = f32 MFMA peak = 157.3 TF); achieved = "
+                 "reference work model FLOPs per launch "
+                 f"({flops / nvis:.0f} FLOP/vis x {nvis} vis) / mean "
+                 "kernel duration (HIP events on the launch stream)"),
+    }
+    roofline_hbm = {
+        "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+        "achieved": round(nbytes / t_dom / 1e9, 2),
+        "frac": round(nbytes / t_dom / 1e9 / HBM_PEAK_GBS, 4),
+        "note": ("reference byte model (common.cpp:131-159, "
+                 f"{nbytes / nvis:.2f} B/vis); AI = {flops / nbytes:.0f} "
+                 "FLOP/B, so <= ~5.5% by construction"),
+    }
+
+    result = {
+        "metric": METRIC,
+        "value": round(world * nvis / sec_per_step / 1e6, 2),
+        "unit": "Mvis/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(sec_per_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference generators app/common/init.cpp, srand(0))",
+        "config": {
+            "workload": (f"{args.workload}: NR_STATIONS={st} "
+                         f"NR_TIMESLOTS={ts} NR_TIMESTEPS_SUBGRID={T} "
+                         f"NR_CHANNELS={C} SUBGRID_SIZE={S} GRID_SIZE={G}"),
+            "baseline_config": ("configs[1]" if args.workload == "default"
+                                else {"c256": "configs[2]",
+                                      "s64": "configs[4]"}[args.workload]),
+            "nr_subgrids_per_gpu": ns,
+            "visibilities_per_gpu_per_step": nvis,
+            "step": "gridder + degridder over the batch",
+            "parallelism": f"subgrid-sharded x{world}, no data-path collective",
+        },
+        "gridder_mvis_s": round(world * nvis / t_grid / 1e6, 2),
+        "degridder_mvis_s": round(world * nvis / t_degrid / 1e6, 2),
+        "kernels": kernels,
+        "roofline": roofline,
+        "roofline_hbm": roofline_hbm,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w, a, args.cpu_sample_subgrids)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.finalize()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,10 +2,10 @@
 //
 // Every expression below states its evaluation precision explicitly so the
 // numbers match the reference generators (app/common/init.cpp) regardless of
-// the host compiler: float/double conversions are spelled out and the one
-// multiply-add the reference build fuses (the point-source phase
-// u*l + v*m, init.cpp:66-69) is written as fmaf.  Built with
-// -ffp-contract=off.
+// the host compiler: float/double conversions are spelled out and the
+// multiply-adds the reference build fuses (the ellipse radii and A-term scale
+// in double, the point-source phase u*l + v*m in float) are written as
+// fma/fmaf.  Built with -ffp-contract=off.
 #include "init.hpp"
 
 #include <cmath>
@@ -34,15 +34,19 @@ void initialize_uvw(unsigned int grid_size,
   const double half = static_cast<double>(grid_size / 2);
   const float deg_per_step = 360.0f / static_cast<float>(steps);
   for (size_t r = 0; r < rows; ++r) {
-    const float ru = static_cast<float>(half + draw_unit() * half);
-    const float rv = static_cast<float>(half + draw_unit() * half);
+    // The reference build (GCC 11, -O3 -march=native) fuses the double
+    // `half + u * half` (init.cpp:11-14) and -- as its disassembly shows --
+    // keeps the radii in double: the `float radius_u` rounding is elided
+    // and u = (float)(radius * cos(angle * pi)) is formed from the double.
+    const double ru = std::fma(draw_unit(), half, half);
+    const double rv = std::fma(draw_unit(), half, half);
     idg::UVWCoordinate<float> *row = uvw.data(r);
     for (size_t t = 0; t < steps; ++t) {
       const float angle = static_cast<float>(
           (static_cast<double>(t) + 0.5) / static_cast<double>(deg_per_step));
       const double a = static_cast<double>(angle) * kPi;
-      row[t].u = static_cast<float>(static_cast<double>(ru) * std::cos(a));
-      row[t].v = static_cast<float>(static_cast<double>(rv) * std::sin(a));
+      row[t].u = static_cast<float>(ru * std::cos(a));
+      row[t].v = static_cast<float>(rv * std::sin(a));
       row[t].w = 0.0f;
     }
   }
@@ -136,7 +140,8 @@ void initialize_aterms(
     for (size_t st = 0; st < stations; ++st)
       for (size_t y = 0; y < S; ++y)
         for (size_t x = 0; x < S; ++x) {
-          const float scale = static_cast<float>(0.8 + draw_unit() * 0.4);
+          // fused in the reference build: fma(u, 0.4, 0.8) (init.cpp:120)
+          const float scale = static_cast<float>(std::fma(draw_unit(), 0.4, 0.8));
           const double value = static_cast<double>(spheroidal(y, x) * scale);
           const float hi = static_cast<float>(value + 0.1);
           const float lo = static_cast<float>(value - 0.2);

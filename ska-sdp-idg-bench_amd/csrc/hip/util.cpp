@@ -310,9 +310,10 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
   IDG_TRY(hipMemcpy(d_sph.ptr, spheroidal, b_sph, h2d));
   IDG_TRY(hipMemcpy(d_at.ptr, aterms, b_at, h2d));
   IDG_TRY(hipMemcpy(d_md.ptr, metadata, b_md, h2d));
-  if (dir == Direction::kGridder)
-    IDG_TRY(hipMemcpy(d_vis.ptr, visibilities, b_vis, h2d));
-  else
+  // The degridder writes only the rows its subgrids reference; uploading
+  // the caller's buffer first leaves every other row as the caller had it.
+  IDG_TRY(hipMemcpy(d_vis.ptr, visibilities, b_vis, h2d));
+  if (dir == Direction::kDegridder)
     IDG_TRY(hipMemcpy(d_sg.ptr, subgrids, b_sg, h2d));
   IDG_TRY(launch(dir, p, d_uvw.ptr, static_cast<const float *>(d_wn.ptr),
                  d_vis.ptr, static_cast<const float *>(d_sph.ptr), d_at.ptr,

@@ -1,0 +1,23 @@
+"""idg_amd -- MI355X-native IDG gridder/degridder (host side).
+
+A Python mirror of the reference's gridder/degridder operator interface over
+the C ABI of libidg_mi355x.so (include/idg_mi355x.h).  Importing this package
+loads the HIP library and raises if it is missing: there is no CPU fallback.
+"""
+from .api import (IMAGE_SIZE, METADATA_DTYPE, NR_CORRELATIONS, W_STEP,
+                  IdgError, abi_version, as_metadata, bytes_gridder,
+                  c_run_degridder, c_run_gridder, degridder_launch,
+                  device_name, flops_gridder, generate, gridder_launch,
+                  kernel_name, nr_subgrids_for, p_run_degridder,
+                  p_run_gridder, validate_metadata)
+from ._lib import LIB_PATH
+from . import shard
+
+__all__ = [
+    "IMAGE_SIZE", "METADATA_DTYPE", "NR_CORRELATIONS", "W_STEP", "IdgError",
+    "abi_version", "as_metadata", "bytes_gridder", "c_run_degridder",
+    "c_run_gridder", "degridder_launch", "device_name", "flops_gridder",
+    "generate", "gridder_launch", "kernel_name", "nr_subgrids_for",
+    "p_run_degridder", "p_run_gridder", "validate_metadata", "LIB_PATH",
+    "shard",
+]

@@ -1,0 +1,282 @@
+"""Python mirror of the reference's gridder/degridder operator interface.
+
+Same names, argument order and meaning as the reference's kernel-TU contract
+(hip::c_run_gridder / hip::c_run_degridder, declared by the harness at
+tests/gridder_common.cpp:13-31 and tests/degridder_common.cpp:13-31) and its
+perf entries (hip::p_run_gridder / hip::p_run_degridder), over the C ABI of
+libidg_mi355x.so.  numpy arrays stand in for the idg::ArrayND objects;
+device-resident variants take torch CUDA tensors (PyTorch is only used as the
+device allocator / stream provider).
+
+Errors: where the reference's C++ entries abort the process (hipCheck ->
+exit, app/HIP/util.cpp:5-15), these raise IdgError carrying the status code
+and message.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib
+
+IMAGE_SIZE = 0.01   # app/common/parameters.hpp:4
+W_STEP = 0.0        # app/common/parameters.hpp:5
+NR_CORRELATIONS = 4
+
+METADATA_DTYPE = np.dtype([("baseline_offset", "<i4"), ("time_offset", "<i4"),
+                           ("nr_timesteps", "<i4"), ("aterm_index", "<i4"),
+                           ("station1", "<u4"), ("station2", "<u4"),
+                           ("x", "<i4"), ("y", "<i4"), ("z", "<i4")])
+assert METADATA_DTYPE.itemsize == 36
+
+
+class IdgError(RuntimeError):
+    def __init__(self, code, what):
+        msg = lib.idg_last_error().decode(errors="replace")
+        super().__init__(f"{what} failed (status {code}): {msg}")
+        self.code = code
+
+
+def _check(code, what):
+    if code != 0:
+        raise IdgError(code, what)
+
+
+def _np_ptr(a, dtype, name, writable=False):
+    if not isinstance(a, np.ndarray):
+        raise TypeError(f"{name} must be a numpy array")
+    if a.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {a.dtype}")
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError(f"{name} must be C-contiguous")
+    if writable and not a.flags["WRITEABLE"]:
+        raise ValueError(f"{name} must be writable")
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def as_metadata(md):
+    """Accept a METADATA_DTYPE array or an int32 [n, 9] array."""
+    md = np.asarray(md)
+    if md.dtype == METADATA_DTYPE:
+        return np.ascontiguousarray(md)
+    md = np.ascontiguousarray(md, dtype=np.int32).reshape(-1, 9)
+    return md.view(METADATA_DTYPE).reshape(-1)
+
+
+def nr_subgrids_for(nr_stations, nr_timeslots):
+    return nr_stations * (nr_stations - 1) // 2 * nr_timeslots
+
+
+# ---------------------------------------------------------------------------
+# Synthetic observation (app/common/init.cpp, harness order, srand(0))
+# ---------------------------------------------------------------------------
+def generate(nr_stations, nr_timeslots, nr_timesteps, nr_channels, grid_size,
+             subgrid_size, want=("uvw", "frequencies", "wavenumbers",
+                                 "visibilities", "spheroidal", "aterms",
+                                 "metadata", "subgrids"), nthreads=8):
+    """Return a dict of numpy arrays holding exactly the inputs the reference
+    harness builds (tests/gridder_common.cpp:87-101).  Shapes:
+      uvw [NS, T, 3] f32; frequencies, wavenumbers [C] f32;
+      visibilities [NS, T, C, 4, 2] f32; spheroidal [S, S] f32;
+      aterms [TS, ST, S, S, 4, 2] f32; metadata [NS] METADATA_DTYPE;
+      subgrids [NS, 4, S, S, 2] f32 (the degridder input ramp)."""
+    ns = nr_subgrids_for(nr_stations, nr_timeslots)
+    S = subgrid_size
+    shapes = {
+        "uvw": ((ns, nr_timesteps, 3), np.float32),
+        "frequencies": ((nr_channels,), np.float32),
+        "wavenumbers": ((nr_channels,), np.float32),
+        "visibilities": ((ns, nr_timesteps, nr_channels, 4, 2), np.float32),
+        "spheroidal": ((S, S), np.float32),
+        "aterms": ((nr_timeslots, nr_stations, S, S, 4, 2), np.float32),
+        "metadata": ((ns,), METADATA_DTYPE),
+        "subgrids": ((ns, 4, S, S, 2), np.float32),
+    }
+    out = {k: np.empty(*shapes[k]) for k in want}
+    ptr = {k: (out[k].ctypes.data_as(ctypes.c_void_p) if k in out else None)
+           for k in shapes}
+    got = lib.idg_generate(nr_stations, nr_timeslots, nr_timesteps,
+                           nr_channels, grid_size, subgrid_size, ptr["uvw"],
+                           ptr["frequencies"], ptr["wavenumbers"],
+                           ptr["visibilities"], ptr["spheroidal"],
+                           ptr["aterms"], ptr["metadata"], ptr["subgrids"],
+                           nthreads)
+    if got < 0:
+        raise IdgError(got, "idg_generate")
+    assert got == ns
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Host-buffer entries: hip::c_run_gridder / hip::c_run_degridder
+# ---------------------------------------------------------------------------
+def _extents(nr_channels, uvw, visibilities, aterms, subgrids, subgrid_size,
+             nr_subgrids, nr_stations):
+    rows = uvw.size // 3
+    if uvw.size % 3:
+        raise ValueError("uvw must hold whole (u, v, w) triplets")
+    if visibilities.size != rows * nr_channels * 8:
+        raise ValueError(
+            f"visibilities must hold rows*nr_channels*4 complex values "
+            f"({rows}*{nr_channels}*4), got {visibilities.size // 2}")
+    per_slot = nr_stations * subgrid_size * subgrid_size * 8
+    if aterms.size % per_slot:
+        raise ValueError("aterms must be [slots][nr_stations][S][S][4] complex")
+    if subgrids.size != nr_subgrids * 4 * subgrid_size * subgrid_size * 2:
+        raise ValueError("subgrids must be [nr_subgrids][4][S][S] complex")
+    return rows, aterms.size // per_slot
+
+
+def c_run_gridder(nr_subgrids, grid_size, subgrid_size, image_size,
+                  w_step_in_lambda, nr_channels, nr_stations, uvw,
+                  wavenumbers, visibilities, spheroidal, aterms, metadata,
+                  subgrids):
+    """Grid visibilities onto subgrids (fills `subgrids` in place)."""
+    md = as_metadata(metadata)
+    rows, slots = _extents(nr_channels, uvw, visibilities, aterms, subgrids,
+                           subgrid_size, nr_subgrids, nr_stations)
+    _check(lib.idg_c_run_gridder(
+        nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
+        nr_channels, nr_stations, _np_ptr(uvw, np.float32, "uvw"), rows,
+        _np_ptr(wavenumbers, np.float32, "wavenumbers"),
+        _np_ptr(visibilities, np.float32, "visibilities"),
+        _np_ptr(spheroidal, np.float32, "spheroidal"),
+        _np_ptr(aterms, np.float32, "aterms"), slots,
+        _np_ptr(md, METADATA_DTYPE, "metadata"),
+        _np_ptr(subgrids, np.float32, "subgrids", True)), "c_run_gridder")
+    return subgrids
+
+
+def c_run_degridder(nr_subgrids, grid_size, subgrid_size, image_size,
+                    w_step_in_lambda, nr_channels, nr_stations, uvw,
+                    wavenumbers, visibilities, spheroidal, aterms, metadata,
+                    subgrids):
+    """Degrid subgrids into visibilities (fills `visibilities` in place)."""
+    md = as_metadata(metadata)
+    rows, slots = _extents(nr_channels, uvw, visibilities, aterms, subgrids,
+                           subgrid_size, nr_subgrids, nr_stations)
+    _check(lib.idg_c_run_degridder(
+        nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
+        nr_channels, nr_stations, _np_ptr(uvw, np.float32, "uvw"), rows,
+        _np_ptr(wavenumbers, np.float32, "wavenumbers"),
+        _np_ptr(visibilities, np.float32, "visibilities", True),
+        _np_ptr(spheroidal, np.float32, "spheroidal"),
+        _np_ptr(aterms, np.float32, "aterms"), slots,
+        _np_ptr(md, METADATA_DTYPE, "metadata"),
+        _np_ptr(subgrids, np.float32, "subgrids")), "c_run_degridder")
+    return visibilities
+
+
+def validate_metadata(nr_subgrids, subgrid_size, nr_channels, nr_stations,
+                      uvw_rows, aterm_slots, metadata):
+    md = as_metadata(metadata)
+    _check(lib.idg_validate_metadata(
+        nr_subgrids, subgrid_size, nr_channels, nr_stations, uvw_rows,
+        aterm_slots, _np_ptr(md, METADATA_DTYPE, "metadata")),
+        "validate_metadata")
+
+
+# ---------------------------------------------------------------------------
+# Device-buffer entries (torch CUDA tensors, asynchronous on a stream)
+# ---------------------------------------------------------------------------
+def _dev_ptr(t, name, dtype=None):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                   w_step_in_lambda, nr_channels, nr_stations, uvw,
+                   wavenumbers, visibilities, spheroidal, aterms, metadata,
+                   subgrids, stream=None):
+    """Enqueue the gridder on device-resident tensors (metadata as int32
+    [NS, 9] tensor or uint8 view of METADATA_DTYPE); returns immediately."""
+    import torch
+    f32 = torch.float32
+    _check(lib.idg_gridder_launch(
+        nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
+        nr_channels, nr_stations, _dev_ptr(uvw, "uvw", f32),
+        _dev_ptr(wavenumbers, "wavenumbers", f32),
+        _dev_ptr(visibilities, "visibilities", f32),
+        _dev_ptr(spheroidal, "spheroidal", f32),
+        _dev_ptr(aterms, "aterms", f32), _dev_ptr(metadata, "metadata"),
+        _dev_ptr(subgrids, "subgrids", f32), _stream_handle(stream)),
+        "gridder_launch")
+
+
+def degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                     w_step_in_lambda, nr_channels, nr_stations, uvw,
+                     wavenumbers, visibilities, spheroidal, aterms, metadata,
+                     subgrids, stream=None):
+    """Enqueue the degridder on device-resident tensors; returns immediately."""
+    import torch
+    f32 = torch.float32
+    _check(lib.idg_degridder_launch(
+        nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
+        nr_channels, nr_stations, _dev_ptr(uvw, "uvw", f32),
+        _dev_ptr(wavenumbers, "wavenumbers", f32),
+        _dev_ptr(visibilities, "visibilities", f32),
+        _dev_ptr(spheroidal, "spheroidal", f32),
+        _dev_ptr(aterms, "aterms", f32), _dev_ptr(metadata, "metadata"),
+        _dev_ptr(subgrids, "subgrids", f32), _stream_handle(stream)),
+        "degridder_launch")
+
+
+# ---------------------------------------------------------------------------
+# Perf entries, device info, work model
+# ---------------------------------------------------------------------------
+def p_run_gridder():
+    """hip::p_run_gridder: env-configured perf run; returns ms per launch."""
+    ms = lib.idg_p_run_gridder()
+    if ms < 0:
+        raise IdgError(-1, "p_run_gridder")
+    return ms
+
+
+def p_run_degridder():
+    ms = lib.idg_p_run_degridder()
+    if ms < 0:
+        raise IdgError(-1, "p_run_degridder")
+    return ms
+
+
+def device_name():
+    buf = ctypes.create_string_buffer(256)
+    n = lib.idg_get_device_name(buf, 256)
+    if n < 0:
+        raise IdgError(n, "get_device_name")
+    return buf.value.decode()
+
+
+def kernel_name(direction, subgrid_size, nr_channels):
+    d = {"gridder": 0, "degridder": 1}.get(direction, direction)
+    return lib.idg_kernel_name(d, subgrid_size, nr_channels).decode()
+
+
+def flops_gridder(nr_channels, nr_timesteps, nr_subgrids, subgrid_size,
+                  nr_correlations=NR_CORRELATIONS):
+    """Reference work model (app/common/common.cpp:100-129); nr_timesteps is
+    the TOTAL number of timesteps, as the reference passes it."""
+    return lib.idg_flops_gridder(nr_channels, nr_timesteps, nr_subgrids,
+                                 subgrid_size, nr_correlations)
+
+
+def bytes_gridder(nr_channels, nr_timesteps, nr_subgrids, subgrid_size,
+                  nr_correlations=NR_CORRELATIONS):
+    return lib.idg_bytes_gridder(nr_channels, nr_timesteps, nr_subgrids,
+                                 subgrid_size, nr_correlations)
+
+
+def abi_version():
+    return lib.idg_abi_version()

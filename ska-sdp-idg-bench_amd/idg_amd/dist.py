@@ -1,0 +1,89 @@
+"""One process per GPU: rank setup and the few collectives the driver needs.
+
+The gridder/degridder data path has no collective (subgrids shard with no
+exchange, idg_amd.shard); torch.distributed is used only for the bench's
+barrier / max-over-ranks timing and for optional gathers of shard outputs.
+Backend "nccl" is RCCL on ROCm (over xGMI); "gloo" runs the same code on CPU.
+"""
+import os
+
+import torch
+import torch.distributed as torch_dist
+
+
+def env_rank():
+    """(rank, local_rank, world_size) from the torchrun environment."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init(backend=None):
+    """Initialise the process group when WORLD_SIZE > 1.  Returns
+    (rank, local_rank, world_size)."""
+    rank, local_rank, world = env_rank()
+    if world > 1 and not torch_dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            torch_dist.init_process_group(backend, rank=rank, world_size=world,
+                                          device_id=torch.device("cuda",
+                                                                 local_rank))
+        else:
+            torch_dist.init_process_group(backend, rank=rank, world_size=world)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    return rank, local_rank, world
+
+
+def _device():
+    if torch_dist.is_initialized() and \
+            torch_dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def barrier():
+    if torch_dist.is_initialized():
+        if torch_dist.get_backend() == "nccl":
+            torch_dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            torch_dist.barrier()
+
+
+def max_over_ranks(value):
+    """Max of a float over all ranks (identity on one process)."""
+    if not torch_dist.is_initialized():
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_device())
+    torch_dist.all_reduce(t, op=torch_dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(value):
+    if not torch_dist.is_initialized():
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_device())
+    torch_dist.all_reduce(t, op=torch_dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_shards(local, counts):
+    """All-gather variable-sized shards along dim 0 (counts[r] rows on rank
+    r); returns the concatenation in rank order on every rank."""
+    if not torch_dist.is_initialized():
+        return local
+    world = torch_dist.get_world_size()
+    width = max(counts) if counts else 0
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    pad[:local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    torch_dist.all_gather(bufs, pad)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+def finalize():
+    if torch_dist.is_initialized():
+        torch_dist.destroy_process_group()

@@ -1,0 +1,82 @@
+"""World-size-2 gloo rehearsal of the multi-GPU path (CPU only).
+
+The subgrid shard plan + rebasing (idg_amd.shard) and the driver's
+collectives (idg_amd.dist: barrier, max-over-ranks, gather of shard outputs)
+run on two CPU processes; the per-shard compute is the CPU oracle standing in
+for the GPU kernel (the oracle is the checker here, not the thing shipped).
+The gathered result must equal a single-process run bit for bit.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ORACLE, PKG
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, result_path):
+    import sys
+    for p in (PKG, ORACLE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import idg_amd
+    from idg_amd import dist, shard
+    import oracle as orc
+    r, _, w = dist.init(backend="gloo")
+    st, ts, T, C, G, S = 4, 3, 6, 3, 256, 16
+    a = idg_amd.generate(st, ts, T, C, G, S)
+    md = a["metadata"]
+    plan = shard.plan_shards(md, w)
+    s0, s1 = plan[r]
+    sub, r0, r1 = shard.shard(md, s0, s1)
+    out = np.zeros((s1 - s0, 4, S, S, 2), np.float32)
+    uvw = np.ascontiguousarray(a["uvw"].reshape(-1, 3)[r0:r1])
+    vis = np.ascontiguousarray(a["visibilities"].reshape(-1, C, 4, 2)[r0:r1])
+    orc.Oracle().gridder(s1 - s0, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st, uvw,
+                         a["wavenumbers"], vis, a["spheroidal"], a["aterms"],
+                         sub, out)
+    counts = [b - a_ for a_, b in plan]
+    full = dist.gather_shards(torch.from_numpy(out), counts)
+    dist.barrier()
+    tmax = dist.max_over_ranks(float(r + 1))
+    tsum = dist.sum_over_ranks(1.0)
+    if r == 0:
+        np.save(result_path, full.numpy())
+        with open(result_path + ".txt", "w") as f:
+            f.write(f"{tmax} {tsum}")
+    dist.finalize()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_sharded_gridder_equals_single_process(tmp_path,
+                                                           oracle_lib):
+    import idg_amd
+    port = _free_port()
+    path = str(tmp_path / "full.npy")
+    mp.start_processes(_worker, args=(2, port, path), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(path)
+    st, ts, T, C, G, S = 4, 3, 6, 3, 256, 16
+    a = idg_amd.generate(st, ts, T, C, G, S)
+    ns = a["metadata"].size
+    ref = np.zeros((ns, 4, S, S, 2), np.float32)
+    oracle_lib.gridder(ns, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st, a["uvw"],
+                       a["wavenumbers"], a["visibilities"], a["spheroidal"],
+                       a["aterms"], a["metadata"], ref)
+    assert np.array_equal(got, ref)
+    tmax, tsum = open(path + ".txt").read().split()
+    assert float(tmax) == 2.0 and float(tsum) == 2.0

@@ -1,0 +1,346 @@
+"""Parity of the MI355X gridder/degridder (run on the GPU box: -m gpu).
+
+Bar: the reference harness metric (tests/test_util.hpp:28-92), normalised RMS
+error <= 1e-5, against (a) the reference's own CPU outputs (tests/golden/) and
+(b) the oracle on the same inputs; at BASELINE.json's full sizes through
+size-independent properties (linearity, gridder/degridder adjointness,
+shard invariance, determinism) plus oracle spot checks of sampled subgrids.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import CASES, REPO, TOLERANCE, load_case
+
+pytestmark = pytest.mark.gpu
+
+HARNESS = os.path.join(REPO, "tests", "harness", "bin")
+
+
+@pytest.fixture(scope="module")
+def idg():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    import idg_amd
+    return idg_amd
+
+
+def _params(p):
+    return (p["nr_subgrids"], p["grid_size"], p["subgrid_size"],
+            p["image_size"], p["w_step_in_lambda"], p["nr_channels"],
+            p["nr_stations"])
+
+
+def _grid(idg, p, a, vis=None, md=None):
+    out = np.zeros_like(a["gridder_out"]) if "gridder_out" in a else \
+        np.zeros((p["nr_subgrids"], 4, p["subgrid_size"], p["subgrid_size"],
+                  2), np.float32)
+    idg.c_run_gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                      a["visibilities"] if vis is None else vis,
+                      a["spheroidal"], a["aterms"],
+                      a["metadata"] if md is None else md, out)
+    return out
+
+
+def _degrid(idg, p, a, sg=None, md=None):
+    out = np.zeros(a["uvw"].shape[:2] + (p["nr_channels"], 4, 2), np.float32)
+    idg.c_run_degridder(*_params(p), a["uvw"], a["wavenumbers"], out,
+                        a["spheroidal"], a["aterms"],
+                        a["metadata"] if md is None else md,
+                        a["subgrids"] if sg is None else sg)
+    return out
+
+
+# --------------------------------------------------------------------------
+# (a)+(b): golden vectors from the reference, and the oracle
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("case", CASES)
+def test_gridder_matches_reference_golden(idg, oracle_lib, case):
+    p, a = load_case(case)
+    g = _grid(idg, p, a)
+    err, nnz = oracle_lib.check_error(g, a["gridder_out"])
+    assert nnz > 0
+    assert err <= TOLERANCE, f"{case}: gridder error {err}"
+    # every output written (the spheroidal zeroes row/col S/2 only)
+    assert np.isfinite(g).all()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_degridder_matches_reference_golden(idg, oracle_lib, case):
+    p, a = load_case(case)
+    d = _degrid(idg, p, a)
+    err, nnz = oracle_lib.check_error(d, a["degridder_out"])
+    assert nnz > 0
+    assert err <= TOLERANCE, f"{case}: degridder error {err}"
+
+
+@pytest.mark.parametrize("case", ["c_default", "odd"])
+def test_matches_oracle_on_same_inputs(idg, oracle_lib, case):
+    p, a = load_case(case)
+    g = _grid(idg, p, a)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"],
+                       a["metadata"], go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], a["metadata"],
+                         a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+# --------------------------------------------------------------------------
+# Geometry sweep against the oracle (edge cases the reference can express)
+# --------------------------------------------------------------------------
+SWEEP = [
+    # (stations, timeslots, T, C, G, S)
+    (2, 1, 1, 1, 64, 8),        # single timestep, single channel
+    (3, 1, 5, 2, 128, 16),
+    (2, 2, 9, 7, 256, 24),      # S^2 = 576, C odd
+    (2, 1, 13, 9, 512, 40),     # C not a multiple of 4 or 8, S^2 = 1600
+    (2, 1, 3, 5, 1024, 64),     # S = 64 specialisation
+    (2, 1, 33, 12, 1024, 32),   # C = 12 (channel group of 4)
+    (2, 1, 4, 300, 1024, 32),   # many channels (several anchor blocks)
+    (2, 1, 700, 2, 1024, 32),   # many timesteps (> 256 degridder units)
+]
+
+
+@pytest.mark.parametrize("geom", SWEEP)
+def test_geometry_sweep_vs_oracle(idg, oracle_lib, geom):
+    st, ts, T, C, G, S = geom
+    a = idg.generate(st, ts, T, C, G, S)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    g = _grid(idg, p, a)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"],
+                       a["metadata"], go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], a["metadata"],
+                         a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+def test_w_terms_vs_oracle(idg, oracle_lib):
+    # non-zero w and w_step exercise the n-term fusion (row a3 of §8)
+    st, ts, T, C, G, S = 3, 2, 16, 8, 512, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    rng = np.random.default_rng(3)
+    a["uvw"][..., 2] = rng.uniform(-200, 200, a["uvw"].shape[:2])
+    md = a["metadata"].copy()
+    md["z"] = rng.integers(-3, 4, md.size)
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=2.5, nr_channels=C,
+             nr_stations=st)
+    g = _grid(idg, p, a, md=md)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"], md, go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a, md=md)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], md, a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+def test_empty_and_ragged_subgrids(idg, oracle_lib):
+    # nr_timesteps = 0 subgrids, ragged timestep counts, non-zero
+    # baseline offsets and A-term slots
+    st, ts, T, C, G, S = 3, 2, 10, 4, 256, 16
+    a = idg.generate(st, ts, T, C, G, S)
+    md = a["metadata"].copy()
+    md["nr_timesteps"] = [0, 10, 3, 7, 0, 1]
+    md["aterm_index"] = [0, 1, 1, 0, 1, 0]
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    g = _grid(idg, p, a, md=md)
+    assert not g[0].any() and not g[4].any()  # empty subgrid -> zeros
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"], md, go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    sentinel = np.float32(7.25)
+    d = np.full(a["uvw"].shape[:2] + (C, 4, 2), sentinel, np.float32)
+    idg.c_run_degridder(*_params(p), a["uvw"], a["wavenumbers"], d,
+                        a["spheroidal"], a["aterms"], md, a["subgrids"])
+    do = np.full_like(d, sentinel)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], md, a["subgrids"])
+    # rows not referenced stay untouched, referenced rows match
+    assert np.array_equal(d == sentinel, do == sentinel)
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+def test_device_launch_matches_host_entry(idg):
+    import torch
+    p, a = load_case("c_default")
+    g_host = _grid(idg, p, a)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+           for k, v in a.items() if k != "metadata"}
+    md = torch.from_numpy(a["metadata"].astype(np.int32)).cuda()
+    out = torch.zeros_like(dev["gridder_out"])
+    idg.gridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                       dev["visibilities"], dev["spheroidal"], dev["aterms"],
+                       md, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), g_host)
+    vis = torch.zeros_like(dev["degridder_out"])
+    idg.degridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], vis,
+                         dev["spheroidal"], dev["aterms"], md,
+                         dev["subgrids"])
+    torch.cuda.synchronize()
+    assert np.array_equal(vis.cpu().numpy(), _degrid(idg, p, a))
+
+
+# --------------------------------------------------------------------------
+# Full BASELINE sizes: size-independent properties + sampled oracle checks
+# --------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def full(idg):
+    """BASELINE.json configs[1]: NR_STATIONS=50, NR_TIMESLOTS=20, T=128,
+    C=16, S=32, G=1024 -> 24,500 subgrids, 50.2 M visibilities, on device."""
+    import torch
+    st, ts, T, C, G, S = 50, 20, 128, 16, 1024, 32
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    dev = {k: torch.from_numpy(v).cuda() for k, v in a.items()
+           if k not in ("metadata", "frequencies")}
+    dev["metadata"] = torch.from_numpy(
+        a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
+    return p, a, dev
+
+
+def _dgrid(idg, p, dev, vis, md=None):
+    import torch
+    out = torch.empty((p["nr_subgrids"], 4, p["subgrid_size"],
+                       p["subgrid_size"], 2), dtype=torch.float32,
+                      device="cuda")
+    idg.gridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], vis,
+                       dev["spheroidal"], dev["aterms"],
+                       dev["metadata"] if md is None else md, out)
+    return out
+
+
+def _ddegrid(idg, p, dev, sg):
+    import torch
+    out = torch.empty_like(dev["visibilities"])
+    idg.degridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], out,
+                         dev["spheroidal"], dev["aterms"], dev["metadata"], sg)
+    return out
+
+
+def test_full_size_sampled_subgrids_vs_oracle(idg, oracle_lib, full):
+    import torch
+    p, a, dev = full
+    g = _dgrid(idg, p, dev, dev["visibilities"]).cpu().numpy()
+    d = _ddegrid(idg, p, dev, dev["subgrids"]).cpu().numpy()
+    torch.cuda.synchronize()
+    T = a["uvw"].shape[1]
+    for s in (0, 1, 12_345, p["nr_subgrids"] - 1):
+        md = a["metadata"][s:s + 1]
+        go = np.zeros_like(g[s:s + 1])
+        q = dict(p, nr_subgrids=1)
+        oracle_lib.gridder(*_params(q), a["uvw"], a["wavenumbers"],
+                           a["visibilities"], a["spheroidal"], a["aterms"],
+                           md, go)
+        assert oracle_lib.check_error(g[s:s + 1], go)[0] <= TOLERANCE, s
+        do = np.zeros_like(a["visibilities"][s:s + 1])
+        # the oracle indexes rows from md[0]; pass this subgrid's rows only
+        md0 = md.copy()
+        md0["time_offset"] = 0
+        oracle_lib.degridder(*_params(q), np.ascontiguousarray(a["uvw"][s]),
+                             a["wavenumbers"], do, a["spheroidal"],
+                             a["aterms"], md0,
+                             np.ascontiguousarray(a["subgrids"][s:s + 1]))
+        assert oracle_lib.check_error(d[s:s + 1], do)[0] <= TOLERANCE, s
+        assert int(md["nr_timesteps"][0]) == T
+
+
+def test_full_size_linearity(idg, full):
+    import torch
+    p, a, dev = full
+    v1 = dev["visibilities"]
+    v2 = torch.roll(v1, shifts=1, dims=0).contiguous()
+    g1 = _dgrid(idg, p, dev, v1).double()
+    g2 = _dgrid(idg, p, dev, v2).double()
+    g12 = _dgrid(idg, p, dev, (v1 + 2.0 * v2).contiguous()).double()
+    rel = ((g12 - (g1 + 2.0 * g2)).norm() / g12.norm()).item()
+    assert rel < 1e-5, rel
+
+
+def test_full_size_adjointness(idg, full):
+    # the degridder is the adjoint of the gridder: <G v, P> = <v, D P>
+    # (A1^H X A2 vs A1 P A2^H, phases of opposite sign)
+    import torch
+    p, a, dev = full
+    gv = _dgrid(idg, p, dev, dev["visibilities"]).double()
+    dp = _ddegrid(idg, p, dev, dev["subgrids"]).double()
+    v = dev["visibilities"].double()
+    P = dev["subgrids"].double()
+
+    def inner(x, y):  # Re <x, y> for interleaved complex
+        return (x * y).sum().item()
+
+    lhs, rhs = inner(gv, P), inner(v, dp)
+    # scale by the Cauchy-Schwarz bound of either side
+    scale = min(gv.norm().item() * P.norm().item(),
+                v.norm().item() * dp.norm().item())
+    assert abs(lhs - rhs) / scale < 1e-6, (lhs, rhs, scale)
+
+
+def test_full_size_deterministic_and_shard_invariant(idg, full):
+    import torch
+    from idg_amd import shard
+    p, a, dev = full
+    g = _dgrid(idg, p, dev, dev["visibilities"])
+    g_again = _dgrid(idg, p, dev, dev["visibilities"])
+    assert torch.equal(g, g_again)
+    parts = []
+    for s0, s1 in shard.plan_shards(a["metadata"], 3):
+        md, r0, r1 = shard.shard(a["metadata"], s0, s1)
+        q = dict(p, nr_subgrids=s1 - s0)
+        sub = {"uvw": dev["uvw"].reshape(-1, 3)[r0:r1].contiguous(),
+               "wavenumbers": dev["wavenumbers"],
+               "spheroidal": dev["spheroidal"], "aterms": dev["aterms"],
+               "metadata": torch.from_numpy(
+                   md.view(np.int32).reshape(-1, 9).copy()).cuda()}
+        vis = dev["visibilities"].reshape(-1, p["nr_channels"], 4, 2)[r0:r1]
+        parts.append(_dgrid(idg, q, sub, vis.contiguous()))
+    assert torch.equal(torch.cat(parts), g)
+
+
+# --------------------------------------------------------------------------
+# The reference-style harness executables (hip-<kernel> -c)
+# --------------------------------------------------------------------------
+HARNESS_ENVS = [
+    {},
+    {"SUBGRID_SIZE": "64", "NR_TIMESTEPS_SUBGRID": "32"},
+    {"NR_CHANNELS": "256", "NR_TIMESTEPS_SUBGRID": "16"},
+    {"SUBGRID_SIZE": "24", "NR_STATIONS": "3", "NR_CHANNELS": "5"},
+]
+
+
+@pytest.mark.parametrize("exe", ["hip-gridder_mi355x", "hip-degridder_mi355x"])
+@pytest.mark.parametrize("env", HARNESS_ENVS,
+                         ids=["default", "s64", "c256", "s24"])
+def test_harness_correctness_mode(exe, env):
+    path = os.path.join(HARNESS, exe)
+    assert os.path.exists(path), "build the harness: make -C tests/harness"
+    r = subprocess.run([path, "-c"], env=dict(os.environ, IDG_QUIET="1",
+                                              **env),
+                       capture_output=True, text=True, timeout=300)
+    assert ">>> Result PASSED" in r.stdout, r.stdout[-2000:] + r.stderr
+    assert r.returncode == 0
