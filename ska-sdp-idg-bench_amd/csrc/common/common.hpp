@@ -7,8 +7,17 @@
 // reference does at app/HIP/util.cpp:337-343).
 #pragma once
 
+#include <algorithm>
+#include <cmath>
+#include <complex>
 #include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <iomanip>
+#include <iostream>
 #include <string>
+#include <vector>
 
 #include "init.hpp"
 #include "parameters.hpp"

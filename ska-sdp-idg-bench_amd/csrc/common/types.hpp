@@ -66,19 +66,26 @@ T *allocate_memory(size_t n) {
   return static_cast<T *>(ptr);
 }
 
-// Rank-R array.  dims_[0] is the outermost dimension, dims_[R-1] the
-// innermost ("x").  Owning arrays free their buffer; views do not.
+// Rank-R array, row-major, outermost index first in every accessor.
+//
+// Binary layout and symbol names are those of the reference's classes
+// (types.hpp:59-356): a vtable, then the extents in the reference's member
+// order (Array1D: x; Array2D: x, y; Array3D: x, y, z; Array4D: w, z, y, x),
+// then the ownership flag and the buffer pointer; Array1D..Array4D are
+// distinct class templates (not aliases), so a C++ entry point compiled
+// against either header mangles identically and objects can be passed across.
 template <class T, int R>
 class ArrayND {
   static_assert(R >= 1 && R <= 4, "rank 1..4");
 
  public:
-  ArrayND() { dims_.fill(0); }
+  ArrayND() { ext_.fill(0); }
 
   template <class... D, typename = std::enable_if_t<
                             sizeof...(D) == R &&
                             (std::is_integral<D>::value && ...)>>
-  explicit ArrayND(D... dims) : dims_{static_cast<size_t>(dims)...} {
+  explicit ArrayND(D... dims) {
+    set_dims({static_cast<size_t>(dims)...});
     owned_ = count() > 0;
     buf_ = allocate_memory<T>(count());
   }
@@ -86,14 +93,15 @@ class ArrayND {
   template <class... D, typename = std::enable_if_t<
                             sizeof...(D) == R &&
                             (std::is_integral<D>::value && ...)>>
-  ArrayND(T *data, D... dims)
-      : dims_{static_cast<size_t>(dims)...}, owned_(false), buf_(data) {}
+  ArrayND(T *data, D... dims) : owned_(false), buf_(data) {
+    set_dims({static_cast<size_t>(dims)...});
+  }
 
   ArrayND(const ArrayND &) = delete;
   ArrayND &operator=(const ArrayND &) = delete;
 
   ArrayND(ArrayND &&o) noexcept
-      : dims_(o.dims_), owned_(o.owned_), buf_(o.buf_) {
+      : ext_(o.ext_), owned_(o.owned_), buf_(o.buf_) {
     o.buf_ = nullptr;
     o.owned_ = false;
   }
@@ -101,7 +109,7 @@ class ArrayND {
   ArrayND &operator=(ArrayND &&o) noexcept {
     if (this != &o) {
       release();
-      dims_ = o.dims_;
+      ext_ = o.ext_;
       owned_ = o.owned_;
       buf_ = o.buf_;
       o.buf_ = nullptr;
@@ -116,8 +124,11 @@ class ArrayND {
   template <class... I>
   T *data(I... idx) const {
     static_assert(sizeof...(I) <= R, "too many indices");
-    return buf_ + offset_of(std::array<size_t, sizeof...(I)>{
-                      static_cast<size_t>(idx)...});
+    const size_t ix[R + 1] = {static_cast<size_t>(idx)..., 0};
+    size_t off = 0;
+    for (int d = 0; d < R; ++d)
+      off = off * dim(d) + (d < static_cast<int>(sizeof...(I)) ? ix[d] : 0);
+    return buf_ + off;
   }
 
   template <class... I>
@@ -132,10 +143,10 @@ class ArrayND {
   }
 
   // Reference accessor names: x = innermost ... w = outermost of a 4-D array.
-  size_t get_x_dim() const { return dims_[R - 1]; }
-  size_t get_y_dim() const { return inner(1); }
-  size_t get_z_dim() const { return inner(2); }
-  size_t get_w_dim() const { return inner(3); }
+  size_t get_x_dim() const { return dim(R - 1); }
+  size_t get_y_dim() const { return R >= 2 ? dim(R - 2) : 1; }
+  size_t get_z_dim() const { return R >= 3 ? dim(R - 3) : 1; }
+  size_t get_w_dim() const { return R >= 4 ? dim(R - 4) : 1; }
 
   size_t size() const { return count(); }
   size_t bytes() const { return count() * sizeof(T); }
@@ -148,18 +159,16 @@ class ArrayND {
   }
 
  protected:
+  // Storage slot of outermost-first dimension d (reference member order).
+  static constexpr int slot(int d) { return R == 4 ? d : R - 1 - d; }
+  size_t dim(int d) const { return ext_[slot(d)]; }
+  void set_dims(std::array<size_t, R> outer_first) {
+    for (int d = 0; d < R; ++d) ext_[slot(d)] = outer_first[d];
+  }
   size_t count() const {
     size_t n = 1;
-    for (size_t d : dims_) n *= d;
+    for (size_t e : ext_) n *= e;
     return n;
-  }
-  size_t inner(int k) const { return R - 1 - k >= 0 ? dims_[R - 1 - k] : 1; }
-  template <size_t K>
-  size_t offset_of(const std::array<size_t, K> &idx) const {
-    size_t off = 0;
-    for (int d = 0; d < R; ++d)
-      off = off * dims_[d] + (static_cast<size_t>(d) < K ? idx[d] : 0);
-    return off;
   }
   void release() {
     if (owned_) free(buf_);
@@ -167,24 +176,40 @@ class ArrayND {
     owned_ = false;
   }
 
-  std::array<size_t, R> dims_{};
+  std::array<size_t, R> ext_{};
   bool owned_ = false;
   T *buf_ = nullptr;
 };
 
-template <class T>
-using Array1D = ArrayND<T, 1>;
-template <class T>
-using Array2D = ArrayND<T, 2>;
-template <class T>
-using Array3D = ArrayND<T, 3>;
-template <class T>
-using Array4D = ArrayND<T, 4>;
+#define IDG_ARRAY_CLASS(NAME, RANK)                                  \
+  template <class T>                                                 \
+  class NAME : public ArrayND<T, RANK> {                             \
+   public:                                                           \
+    using ArrayND<T, RANK>::ArrayND;                                 \
+    NAME() = default;                                                \
+    NAME(NAME &&) noexcept = default;                                \
+    NAME &operator=(NAME &&) noexcept = default;                     \
+  };
+
+IDG_ARRAY_CLASS(Array1D, 1)
+IDG_ARRAY_CLASS(Array2D, 2)
+IDG_ARRAY_CLASS(Array3D, 3)
+IDG_ARRAY_CLASS(Array4D, 4)
+#undef IDG_ARRAY_CLASS
+
+// Layout checks against the reference classes' member order.
+static_assert(sizeof(Array1D<float>) == 32, "Array1D layout");
+static_assert(sizeof(Array2D<float>) == 40, "Array2D layout");
+static_assert(sizeof(Array3D<float>) == 48, "Array3D layout");
+static_assert(sizeof(Array4D<float>) == 56, "Array4D layout");
 
 // The reference declares (but never uses) a Grid type; kept for API parity.
 class Grid : public Array4D<std::complex<float>> {
  public:
   using Array4D<std::complex<float>>::Array4D;
+  explicit Grid(Array4D<std::complex<float>> &array)
+      : Array4D<std::complex<float>>(array.data(), 1, array.get_z_dim(),
+                                     array.get_y_dim(), array.get_x_dim()) {}
 };
 
 }  // namespace idg

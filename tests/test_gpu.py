@@ -344,3 +344,26 @@ def test_harness_correctness_mode(exe, env):
                        capture_output=True, text=True, timeout=300)
     assert ">>> Result PASSED" in r.stdout, r.stdout[-2000:] + r.stderr
     assert r.returncode == 0
+
+
+# --------------------------------------------------------------------------
+# The REFERENCE's own harness sources (tests/{gridder,degridder}_common.cpp,
+# unmodified, compiled where they lie by oracle/Makefile) linked against the
+# reference's own CPU library and libidg_mi355x.so: the drop-in end to end.
+# --------------------------------------------------------------------------
+REF_HARNESS = os.path.join(REPO, "oracle", "_ref")
+
+
+@pytest.mark.parametrize("exe", ["hip-gridder_mi355x", "hip-degridder_mi355x"])
+@pytest.mark.parametrize("env", HARNESS_ENVS[:3], ids=["default", "s64",
+                                                       "c256"])
+def test_reference_harness_unmodified(exe, env):
+    path = os.path.join(REF_HARNESS, exe)
+    if not os.path.exists(path):
+        pytest.skip("oracle/_ref harness not built (needs /root/reference "
+                    "at build time)")
+    r = subprocess.run([path, "-c"], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=300)
+    # the reference harness exits 0 even on FAILED; the verdict is stdout
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert ">>> Result PASSED" in r.stdout, r.stdout[-3000:]
