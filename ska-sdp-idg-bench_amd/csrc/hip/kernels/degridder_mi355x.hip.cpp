@@ -21,6 +21,9 @@
 //  * phase reduction as in the gridder: per (lane, pixel) the first channel's
 //    phase is converted to revolutions with a Dekker-split 1/(2*pi), the
 //    other channels of the group are exact offsets from it;
+//  * mirror pixels (even S, w = 0, w_offset = 0): phase(S-1-y, S-1-x) =
+//    -phase(y, x) exactly, so each sin/cos pair serves a pixel pair; the
+//    table then holds pairs (P'(base), P'(mirror), geometry(base));
 //  * 16 v_fma_f32 per (pixel, t, c) complex 4-correlation MAC.
 #include <hip/hip_runtime.h>
 
@@ -30,7 +33,54 @@
 
 namespace idg_mi355x {
 
-constexpr int kChunk = 1024;  // pixels per LDS table chunk (48 KiB)
+constexpr int kChunk = 1024;  // general path: pixels per LDS table chunk
+constexpr int kPairChunk = 512;  // mirror path: pixel pairs per chunk
+
+namespace {
+
+// sum += pixel * phasor for 4 correlations (pa = xx|xy, pb = yx|yy).
+__device__ __forceinline__ void cmac4(float *a, const float4 &pa,
+                                      const float4 &pb, float cs, float sn) {
+  a[0] = fma_(pa.x, cs, a[0]); a[0] = fma_(-pa.y, sn, a[0]);
+  a[1] = fma_(pa.x, sn, a[1]); a[1] = fma_(pa.y, cs, a[1]);
+  a[2] = fma_(pa.z, cs, a[2]); a[2] = fma_(-pa.w, sn, a[2]);
+  a[3] = fma_(pa.z, sn, a[3]); a[3] = fma_(pa.w, cs, a[3]);
+  a[4] = fma_(pb.x, cs, a[4]); a[4] = fma_(-pb.y, sn, a[4]);
+  a[5] = fma_(pb.x, sn, a[5]); a[5] = fma_(pb.y, cs, a[5]);
+  a[6] = fma_(pb.z, cs, a[6]); a[6] = fma_(-pb.w, sn, a[6]);
+  a[7] = fma_(pb.z, sn, a[7]); a[7] = fma_(pb.w, cs, a[7]);
+}
+
+// P' = A1 * (sph * P) * A2^H of pixel p, and its geometry.
+__device__ __forceinline__ void pixel_entry(
+    int p, int S, int npix, float image_size, const SubgridSetup &g,
+    int nr_stations, const float *__restrict__ spheroidal,
+    const float2 *__restrict__ aterms, const float2 *__restrict__ sg,
+    float4 &pa, float4 &pb, float4 &geo) {
+  const int y = p / S, x = p - (p / S) * S;
+  const float sph = spheroidal[p];
+  idg::cfloat pix[4], a1[4], a2[4];
+#pragma unroll
+  for (int cr = 0; cr < 4; ++cr) {
+    const float2 v = sg[static_cast<size_t>(cr) * npix + p];
+    pix[cr] = {sph * v.x, sph * v.y};
+  }
+  load_jones(aterm_ptr(aterms, nr_stations, S, g.aterm_index, g.station1, y,
+                       x), a1);
+  load_jones(aterm_ptr(aterms, nr_stations, S, g.aterm_index, g.station2, y,
+                       x), a2);
+  idg::apply_aterm_degridder(pix, a1, a2);
+  const float l = idg::compute_l(x, S, image_size);
+  const float m = idg::compute_m(y, S, image_size);
+  const float n = idg::compute_n(l, m);
+  // phase_offset = fma(u_o, l, v_o*m) + w_o*n (degridder fusion)
+  const float poff = fma_(g.u_offset, l, g.v_offset * m) + g.w_offset * n;
+  pa = make_float4(pix[0].re, pix[0].im, pix[1].re, pix[1].im);
+  pb = make_float4(pix[2].re, pix[2].im, pix[3].re, pix[3].im);
+  geo = make_float4(l, m, n, poff);
+}
+
+}  // namespace
 
 template <int S_CT, int CG>
 __global__ void __launch_bounds__(kBlock)
@@ -44,8 +94,11 @@ __global__ void __launch_bounds__(kBlock)
                             const float2 *__restrict__ aterms,
                             const idg::Metadata *__restrict__ metadata,
                             const float2 *__restrict__ subgrids) {
-  // [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l, m, n, phase_offset)
+  // general: [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l,m,n,poff)
+  // mirror : [pair][0..1] = P'(base), [pair][2..3] = P'(mirror),
+  //          [pair][4] = geometry of the base pixel
   __shared__ float4 table[kChunk * 3];
+  static_assert(kPairChunk * 5 <= kChunk * 3, "table size");
 
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
@@ -53,9 +106,11 @@ __global__ void __launch_bounds__(kBlock)
   const int tid = threadIdx.x;
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);
+  const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const int C = nr_channels;
   const int ncg = (C + CG - 1) / CG;
   const int nunits = g.nr_timesteps * ncg;
+  const bool mirror_ok = (S % 2 == 0) && g.w_offset == 0.0f;
 
   for (int ubase = 0; ubase < nunits; ubase += kBlock) {
     const int unit = min(ubase + tid, nunits - 1);
@@ -73,63 +128,73 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[j][q] = 0.0f;
 
-    for (int pbase = 0; pbase < npix; pbase += kChunk) {
-      const int cnt = min(kChunk, npix - pbase);
-      __syncthreads();  // previous chunk fully consumed
-      for (int q = tid; q < cnt; q += kBlock) {
-        const int p = pbase + q;
-        const int y = p / S, x = p - (p / S) * S;
-        const float sph = spheroidal[p];
-        idg::cfloat pix[4], a1[4], a2[4];
-        const float2 *src = subgrids + static_cast<size_t>(s) * 4 * npix + p;
-#pragma unroll
-        for (int cr = 0; cr < 4; ++cr) {
-          const float2 v = src[static_cast<size_t>(cr) * npix];
-          pix[cr] = {sph * v.x, sph * v.y};
-        }
-        load_jones(aterm_ptr(aterms, nr_stations, S, g.aterm_index,
-                             g.station1, y, x), a1);
-        load_jones(aterm_ptr(aterms, nr_stations, S, g.aterm_index,
-                             g.station2, y, x), a2);
-        idg::apply_aterm_degridder(pix, a1, a2);
-        const float l = idg::compute_l(x, S, image_size);
-        const float m = idg::compute_m(y, S, image_size);
-        const float n = idg::compute_n(l, m);
-        // phase_offset = fma(u_o, l, v_o*m) + w_o*n (degridder fusion)
-        const float poff =
-            fma_(g.u_offset, l, g.v_offset * m) + g.w_offset * n;
-        table[3 * q + 0] = make_float4(pix[0].re, pix[0].im, pix[1].re,
-                                       pix[1].im);
-        table[3 * q + 1] = make_float4(pix[2].re, pix[2].im, pix[3].re,
-                                       pix[3].im);
-        table[3 * q + 2] = make_float4(l, m, n, poff);
-      }
-      __syncthreads();
+    // Workgroup-uniform: every unit of this pass has w = 0.
+    const bool mirror = __syncthreads_and(mirror_ok && c.w == 0.0f);
 
-      for (int q = 0; q < cnt; ++q) {
-        const float4 pa = table[3 * q + 0];
-        const float4 pb = table[3 * q + 1];
-        const float4 geo = table[3 * q + 2];
-        // phase_index = fma(u, l, v*m) + w*n (degridder fusion)
-        const float pidx = fma_(c.u, geo.x, c.v * geo.y) + c.w * geo.z;
-        const float A = fma_(pidx, k[0], -geo.w);
-        const float R = revolutions(A);
+    if (mirror) {
+      // phase(mirror pixel) = -phase(base pixel) exactly.
+      const int half = npix / 2;
+      for (int pbase = 0; pbase < half; pbase += kPairChunk) {
+        const int cnt = min(kPairChunk, half - pbase);
+        __syncthreads();
+        for (int q = tid; q < cnt; q += kBlock) {
+          const int b = pbase + q;
+          float4 pa, pb, geo, ma, mb, mgeo;
+          pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
+                      aterms, sg, pa, pb, geo);
+          pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
+                      spheroidal, aterms, sg, ma, mb, mgeo);
+          table[5 * q + 0] = pa;
+          table[5 * q + 1] = pb;
+          table[5 * q + 2] = ma;
+          table[5 * q + 3] = mb;
+          table[5 * q + 4] = geo;
+        }
+        __syncthreads();
+        for (int q = 0; q < cnt; ++q) {
+          const float4 pa = table[5 * q + 0], pb = table[5 * q + 1];
+          const float4 ma = table[5 * q + 2], mb = table[5 * q + 3];
+          const float4 geo = table[5 * q + 4];
+          // phase_index = fma(u, l, v*m) + w*n with w = 0
+          const float pidx = fma_(c.u, geo.x, c.v * geo.y);
+          const float A = fma_(pidx, k[0], -geo.w);
+          const float R = revolutions(A);
 #pragma unroll
-        for (int j = 0; j < CG; ++j) {
-          const float ph = fma_(pidx, k[j], -geo.w);
-          const float r = fma_(ph - A, kInv2PiHi, R);
-          float sn, cs;
-          sincos_rev(r, &sn, &cs);
-          float *a = acc[j];
-          // sum += pixel * phasor
-          a[0] = fma_(pa.x, cs, a[0]); a[0] = fma_(-pa.y, sn, a[0]);
-          a[1] = fma_(pa.x, sn, a[1]); a[1] = fma_(pa.y, cs, a[1]);
-          a[2] = fma_(pa.z, cs, a[2]); a[2] = fma_(-pa.w, sn, a[2]);
-          a[3] = fma_(pa.z, sn, a[3]); a[3] = fma_(pa.w, cs, a[3]);
-          a[4] = fma_(pb.x, cs, a[4]); a[4] = fma_(-pb.y, sn, a[4]);
-          a[5] = fma_(pb.x, sn, a[5]); a[5] = fma_(pb.y, cs, a[5]);
-          a[6] = fma_(pb.z, cs, a[6]); a[6] = fma_(-pb.w, sn, a[6]);
-          a[7] = fma_(pb.z, sn, a[7]); a[7] = fma_(pb.w, cs, a[7]);
+          for (int j = 0; j < CG; ++j) {
+            const float ph = fma_(pidx, k[j], -geo.w);
+            const float r = fma_(ph - A, kInv2PiHi, R);
+            float sn, cs;
+            sincos_rev(r, &sn, &cs);
+            cmac4(acc[j], pa, pb, cs, sn);
+            cmac4(acc[j], ma, mb, cs, -sn);
+          }
+        }
+      }
+    } else {
+      for (int pbase = 0; pbase < npix; pbase += kChunk) {
+        const int cnt = min(kChunk, npix - pbase);
+        __syncthreads();  // previous chunk fully consumed
+        for (int q = tid; q < cnt; q += kBlock)
+          pixel_entry(pbase + q, S, npix, image_size, g, nr_stations,
+                      spheroidal, aterms, sg, table[3 * q + 0],
+                      table[3 * q + 1], table[3 * q + 2]);
+        __syncthreads();
+        for (int q = 0; q < cnt; ++q) {
+          const float4 pa = table[3 * q + 0];
+          const float4 pb = table[3 * q + 1];
+          const float4 geo = table[3 * q + 2];
+          // phase_index = fma(u, l, v*m) + w*n (degridder fusion)
+          const float pidx = fma_(c.u, geo.x, c.v * geo.y) + c.w * geo.z;
+          const float A = fma_(pidx, k[0], -geo.w);
+          const float R = revolutions(A);
+#pragma unroll
+          for (int j = 0; j < CG; ++j) {
+            const float ph = fma_(pidx, k[j], -geo.w);
+            const float r = fma_(ph - A, kInv2PiHi, R);
+            float sn, cs;
+            sincos_rev(r, &sn, &cs);
+            cmac4(acc[j], pa, pb, cs, sn);
+          }
         }
       }
     }
