@@ -1,0 +1,67 @@
+// mfma.hpp -- f16 MFMA helpers for the gridder/degridder complex MAC.
+//
+// The 4-correlation complex multiply-accumulate of IDG is a genuine dense
+// GEMM once the phasors are materialised: O[row][col] += sum_k A[row][k] *
+// B[k][col] with A = phasors (cos/sin rows) and B = visibilities or pixels
+// (8 real components).  v_mfma_f32_16x16x32_f16 does it at 16x the f32 rate;
+// fp32 accuracy is kept with a two-term f16 split of both operands:
+//   a = a_hi + a_lo   (a_hi = f16(a), a_lo = f16(a - a_hi), |err| ~ 2^-22|a|)
+//   A' = [a_hi, a_lo] stacked along K, B' = [b; b] repeated along K,
+//   B columns = [b_hi (8) | b_lo (8)], O = O[:, 0:8] + O[:, 8:16].
+// (measured: tests/probes/mfma_probe.hip)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace idg_mi355x {
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// (hi, lo) of one float: hi = f16(x) (RNE), lo = f16(x - hi).
+__device__ __forceinline__ half2 split_f16(float x) {
+  const _Float16 hi = static_cast<_Float16>(x);
+  const _Float16 lo = static_cast<_Float16>(x - static_cast<float>(hi));
+  half2 r;
+  r.x = hi;
+  r.y = lo;
+  return r;
+}
+
+// Splits the pair (c, s): *hi = (f16(c), f16(s)), *lo = (f16(c - hi.c),
+// f16(s - hi.s)) in 3 instructions (v_cvt_pk_f16_f32 + v_fma_mix{lo,hi}_f16;
+// the residual c - hi.c is exact in f32 and rounded once to f16).
+__device__ __forceinline__ void split_pair(float c, float s, unsigned *hi,
+                                           unsigned *lo) {
+  floatx2 v = {c, s};
+  const f16x2 h = __builtin_convertvector(v, f16x2);
+  const unsigned hu = __builtin_bit_cast(unsigned, h);
+  unsigned lu;
+  asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]"
+               : "=&v"(lu)
+               : "v"(hu), "v"(c));
+  asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] "
+               "op_sel_hi:[1,0,0]"
+               : "+v"(lu)
+               : "v"(hu), "v"(s));
+  *hi = hu;
+  *lo = lu;
+}
+
+__device__ __forceinline__ floatx4 mfma16(const half8 &a, const half8 &b,
+                                          const floatx4 &c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Four packed-f16 dwords as the 8-element MFMA operand.
+__device__ __forceinline__ half8 pack4(unsigned a, unsigned b, unsigned c,
+                                       unsigned d) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 v = {a, b, c, d};
+  return __builtin_bit_cast(half8, v);
+}
+
+}  // namespace idg_mi355x
