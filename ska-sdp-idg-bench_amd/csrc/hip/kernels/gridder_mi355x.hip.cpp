@@ -29,9 +29,13 @@
 //    compiler into v_pk_fma_f32 (2 FMAs per lane per issue on gfx950).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "../util.hpp"
 #include "device.hpp"
 #include "lib-hip.hpp"
+#include "mfma.hpp"
 
 namespace idg_mi355x {
 
@@ -167,11 +171,207 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
   poff = fma_(g.w_offset, n, fma_(g.u_offset, l, g.v_offset * m));
 }
 
+
+// ---------------------------------------------------------------------------
+// MFMA mirror path (even S, w = 0 on every timestep, w_offset = 0).
+//
+// GEMM per 16-pixel tile: O[pixel][col] += sum_k A[pixel][k] * B[k][col],
+//   k = 8 items x {cos_hi, sin_hi, cos_lo, sin_lo}   (v_mfma_f32_16x16x32_f16)
+//   A = phasors of the BASE pixels (VALU: exact phase, revolutions, v_sin /
+//       v_cos, split into f16 hi/lo), B = visibility coefficients (cos row:
+//       V.re | V.im, sin row: -V.im | V.re) with columns [8 hi | 8 lo],
+//   the MIRROR tile reuses A with the sin rows of B negated.
+// Lane l = (group g = l/16, column/pixel l%16).  Lane group g takes timestep
+// t = 4q + g of each timestep quad q, so every lane keeps its own
+// phase_index / anchor in registers and shares nothing across lanes.
+// B fragments of KS_BUF K-steps are built once per workgroup in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kKsBuf = 32;               // K-steps of B fragments per fill
+constexpr unsigned kNegHi = 0x80000000u;  // negates the sin-row f16
+
+template <int PT>
+struct MfmaLds {
+  static constexpr int kObufFloats = 2 * 64 * PT * 16;
+  static constexpr int kBbufWords = kKsBuf * 64 * 2;
+  static constexpr int kWords =
+      (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
+};
+
+// f16 coefficient dword (cos-row, sin-row) of one visibility item for the
+// B column `col` of the lane, pre-scaled by `scale` (a power of two).
+__device__ __forceinline__ unsigned b_coeff(const float2 *__restrict__ vis,
+                                            long long item, int col,
+                                            float scale) {
+  const int pol = (col & 7) >> 1;
+  const float2 v = vis[item * 4 + pol];
+  const float re = v.x * scale, im = v.y * scale;
+  const bool imag_col = col & 1;
+  const float bc = imag_col ? im : re;
+  const float bs = imag_col ? re : -im;
+  unsigned hi, lo;
+  split_pair(bc, bs, &hi, &lo);
+  return (col & 8) ? lo : hi;
+}
+
+template <int S_CT, int PT, int CB>
+__device__ __forceinline__ void grid_mirror_mfma(
+    const SubgridSetup &g, int S, int npix, float image_size, int C,
+    int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
+    const float *__restrict__ wavenumbers,
+    const float2 *__restrict__ visibilities,
+    const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
+    float2 *__restrict__ out, unsigned *lds) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, col = lane & 15;
+  const int half = npix / 2;
+  const int nt = g.nr_timesteps;
+  const int npairs = (C + 1) / 2;
+
+  // Per-subgrid power-of-two scale keeps every visibility inside f16 range.
+  float vmax = 0.0f;
+  {
+    const float4 *v4 = reinterpret_cast<const float4 *>(
+        visibilities + g.time_offset * C * 4);
+    const int n4 = nt * C * 2;
+    for (int i = tid; i < n4; i += kBlock) {
+      const float4 q = v4[i];
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)),
+                               fmaxf(fabsf(q.z), fabsf(q.w))));
+    }
+    for (int off = 32; off > 0; off >>= 1)
+      vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT>::kWords - 8);
+    if (lane == 0) red[wave] = vmax;
+    __syncthreads();
+    vmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  }
+  int e = 0;
+  if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
+  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
+
+  const float2 *vsub = visibilities;  // indexed by absolute item below
+  uint2 *bbuf = reinterpret_cast<uint2 *>(lds);
+  float *obuf = reinterpret_cast<float *>(lds);
+  const int nquads = (nt + 3) / 4;
+  const int quads_per_fill = npairs <= kKsBuf ? kKsBuf / npairs : 1;
+
+  for (int gbase = 0; gbase < half; gbase += 64 * PT) {
+    float lg[PT], mg[PT], pg[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
+      float n_unused;
+      pixel_geometry(b, S, image_size, g, lg[i], mg[i], n_unused, pg[i]);
+    }
+    floatx4 accb[PT], accm[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      accb[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+      accm[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+
+    for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
+      const int nq = min(quads_per_fill, nquads - q0);
+      for (int p0 = 0; p0 < npairs; p0 += kKsBuf) {
+        const int np = min(kKsBuf, npairs - p0);
+        // ---- B fragments for nq quads x np channel pairs -> LDS ----
+        __syncthreads();
+        for (int w = tid; w < nq * np * 64; w += kBlock) {
+          const int lw = w & 63, ks = w >> 6;
+          const int qq = ks / np, jj = ks - qq * np;
+          const int t = (q0 + qq) * 4 + (lw >> 4);
+          const int c0 = 2 * (p0 + jj);
+          uint2 d = make_uint2(0u, 0u);
+          if (t < nt) {
+            const long long item = (g.time_offset + t) * C + c0;
+            d.x = b_coeff(vsub, item, lw & 15, scale);
+            if (c0 + 1 < C) d.y = b_coeff(vsub, item + 1, lw & 15, scale);
+          }
+          bbuf[ks * 64 + lw] = d;
+        }
+        __syncthreads();
+        // ---- MFMA over the buffered K-steps ----
+        for (int qq = 0; qq < nq; ++qq) {
+          const int t = min((q0 + qq) * 4 + grp, nt - 1);
+          const idg::UVWCoordinate<float> c = uvw[g.time_offset + t];
+          float pidx[PT], A[PT], R[PT];
+#pragma unroll
+          for (int i = 0; i < PT; ++i) pidx[i] = fma_(c.u, lg[i], c.v * mg[i]);
+          // channel blocks of CB channels share one phase anchor
+          for (int jb = 0; jb < np; jb += CB / 2) {
+            const int je = min(jb + CB / 2, np);
+            const float ka = wavenumbers[2 * (p0 + jb)];
+#pragma unroll
+            for (int i = 0; i < PT; ++i) {
+              A[i] = fma_(-pidx[i], ka, pg[i]);
+              R[i] = revolutions(A[i]);
+            }
+            for (int jj = jb; jj < je; ++jj) {
+              const int c0 = 2 * (p0 + jj);
+              const float k0 = wavenumbers[c0];
+              const float k1 = wavenumbers[min(c0 + 1, C - 1)];
+              const uint2 bb = bbuf[(qq * np + jj) * 64 + lane];
+              const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
+              const half8 bm = pack4(bb.x ^ kNegHi, bb.x ^ kNegHi,
+                                     bb.y ^ kNegHi, bb.y ^ kNegHi);
+#pragma unroll
+              for (int i = 0; i < PT; ++i) {
+                const float ph0 = fma_(-pidx[i], k0, pg[i]);
+                const float ph1 = fma_(-pidx[i], k1, pg[i]);
+                const float r0 = fma_(ph0 - A[i], kInv2PiHi, R[i]);
+                const float r1 = fma_(ph1 - A[i], kInv2PiHi, R[i]);
+                float s0, c0f, s1, c1f;
+                sincos_rev(r0, &s0, &c0f);
+                sincos_rev(r1, &s1, &c1f);
+                unsigned h0, l0, h1, l1;
+                split_pair(c0f, s0, &h0, &l0);
+                split_pair(c1f, s1, &h1, &l1);
+                const half8 af = pack4(h0, l0, h1, l1);
+                accb[i] = mfma16(af, bf, accb[i]);
+                accm[i] = mfma16(af, bm, accm[i]);
+              }
+            }
+          }
+        }
+      }
+    }
+
+    // ---- epilogue: D tiles -> LDS [pixel][16], hi + lo, A-term, store ----
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lp = (wave * PT + i) * 16 + grp * 4 + r;
+        obuf[lp * 16 + col] = accb[i][r];
+        obuf[(64 * PT + lp) * 16 + col] = accm[i][r];
+      }
+    __syncthreads();
+    for (int q = tid; q < 2 * 64 * PT; q += kBlock) {
+      const bool mir = q >= 64 * PT;
+      const int b = gbase + (mir ? q - 64 * PT : q);
+      if (b >= half) continue;
+      const float4 *o4 = reinterpret_cast<const float4 *>(obuf + q * 16);
+      const float4 h0 = o4[0], h1 = o4[1], l0 = o4[2], l1 = o4[3];
+      float a[8] = {(h0.x + l0.x) * unscale, (h0.y + l0.y) * unscale,
+                    (h0.z + l0.z) * unscale, (h0.w + l0.w) * unscale,
+                    (h1.x + l1.x) * unscale, (h1.y + l1.y) * unscale,
+                    (h1.z + l1.z) * unscale, (h1.w + l1.w) * unscale};
+      store_pixel(a, mir ? npix - 1 - b : b, S, npix, g, nr_stations,
+                  spheroidal, aterms, out);
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // S_CT: subgrid size known at compile time (0 = runtime).
-// PPT : pixels per lane.   CB: channels per phase anchor.
-template <int S_CT, int PPT, int CB>
+// PPT : pixels per lane (VALU paths).   CB: channels per phase anchor.
+// IMPL: mirror-path implementation, 0 = VALU (v_pk_fma MAC), 1 = MFMA.
+// PT  : 16-pixel base tiles per wave in the MFMA path.
+template <int S_CT, int PPT, int CB, int IMPL, int PT>
 __global__ void __launch_bounds__(kBlock)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
                           float image_size, float w_step_in_lambda,
@@ -201,6 +401,14 @@ __global__ void __launch_bounds__(kBlock)
     w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
   const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
                       g.w_offset == 0.0f;
+
+  if (IMPL == 1 && mirror) {
+    __shared__ unsigned lds[MfmaLds<PT>::kWords];
+    grid_mirror_mfma<S_CT, PT, CB>(g, S, npix, image_size, C, nr_stations,
+                                   uvw, wavenumbers, visibilities, spheroidal,
+                                   aterms, out, lds);
+    return;
+  }
 
   if (mirror) {
     // Mirror-pair path: lane owns base pixels b (< npix/2) and npix-1-b.
@@ -267,25 +475,33 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-#define IDG_GRIDDER(S_, PPT_, CB_) \
-  reinterpret_cast<const void *>(&kernel_gridder_mi355x<S_, PPT_, CB_>)
+#define IDG_GRIDDER(S_, PPT_, IMPL_)                                     \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_mi355x<S_, PPT_, 16, IMPL_, 4>)
+
+// IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
+static int gridder_impl() {
+  const char *v = std::getenv("IDG_GRIDDER_IMPL");
+  return (v && std::string(v) == "valu") ? 0 : 1;
+}
 
 KernelChoice select_gridder(const Problem &p) {
   KernelChoice k;
   k.grid = p.nr_subgrids;
   k.block = kBlock;
+  const bool mfma = gridder_impl() == 1;
   switch (p.subgrid_size) {
     case 32:
-      k.func = IDG_GRIDDER(32, 4, 16);
-      k.name = "gridder_mi355x_s32";
+      k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
+      k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
       break;
     case 64:
-      k.func = IDG_GRIDDER(64, 4, 16);
-      k.name = "gridder_mi355x_s64";
+      k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);
+      k.name = mfma ? "gridder_mi355x_s64" : "gridder_mi355x_s64_valu";
       break;
     default:
-      k.func = IDG_GRIDDER(0, 2, 16);
-      k.name = "gridder_mi355x_generic";
+      k.func = mfma ? IDG_GRIDDER(0, 2, 1) : IDG_GRIDDER(0, 2, 0);
+      k.name = mfma ? "gridder_mi355x_generic" : "gridder_mi355x_generic_valu";
       break;
   }
   return k;
