@@ -27,9 +27,13 @@
 //  * 16 v_fma_f32 per (pixel, t, c) complex 4-correlation MAC.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "../util.hpp"
 #include "device.hpp"
 #include "lib-hip.hpp"
+#include "mfma.hpp"
 
 namespace idg_mi355x {
 
@@ -80,9 +84,173 @@ __device__ __forceinline__ void pixel_entry(
   geo = make_float4(l, m, n, poff);
 }
 
+
+// ---------------------------------------------------------------------------
+// MFMA mirror path (even S, w = 0 for every timestep, w_offset = 0).
+//
+// GEMM over pixels: O[item][col] += sum_k A[item][k] * B[k][col] with
+//   rows  = 16 timesteps of one channel (an item tile; CT tiles = CT
+//           channels share each lane's phase_index),
+//   k     = 4 base pixels (one per lane group) x {base, mirror} x
+//           {cos_hi, sin_hi, cos_lo, sin_lo}       (v_mfma_f32_16x16x32_f16)
+//   A     = phasors exp(i*phase(t, c, base pixel)) (VALU, exact phases),
+//           the mirror slot reuses them (phase(mirror) = -phase(base)),
+//   B     = P' coefficients (cos row: P.re | P.im, sin row: -P.im | P.re),
+//           mirror slot with its sin rows negated, columns [8 hi | 8 lo].
+// B fragments and pixel geometry of kPixChunk base pixels live in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kPixChunk = 256;  // base pixels per LDS chunk (64 K-steps)
+constexpr unsigned kNegHi = 0x80000000u;
+
+struct DegridMfmaLds {
+  static constexpr int kGeoWords = kPixChunk * 4;            // float4 each
+  static constexpr int kBfrWords = (kPixChunk / 4) * 64 * 2;  // uint2 each
+  static constexpr int kWords = kGeoWords + kBfrWords + 8;
+};
+
+// (cos-row, sin-row) f16 coefficient dword of complex p for column col.
+__device__ __forceinline__ unsigned p_coeff(float re, float im, int col,
+                                            bool negate_sin) {
+  const bool imag_col = col & 1;
+  const float bc = imag_col ? im : re;
+  float bs = imag_col ? re : -im;
+  if (negate_sin) bs = -bs;
+  unsigned hi, lo;
+  split_pair(bc, bs, &hi, &lo);
+  return (col & 8) ? lo : hi;
+}
+
+template <int S_CT, int CT, int CB>
+__device__ __forceinline__ void degrid_mirror_mfma(
+    const SubgridSetup &g, int S, int npix, float image_size, int C,
+    int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
+    const float *__restrict__ wavenumbers, float2 *__restrict__ visibilities,
+    const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
+    const float2 *__restrict__ sg, unsigned *lds) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, col = lane & 15;
+  const int half = npix / 2;
+  const int nt = g.nr_timesteps;
+
+  // Per-subgrid power-of-two scale of P' (f16 range).
+  float vmax = 0.0f;
+  for (int p = tid; p < npix; p += kBlock) {
+    float4 pa, pb, geo;
+    pixel_entry(p, S, npix, image_size, g, nr_stations, spheroidal, aterms,
+                sg, pa, pb, geo);
+    vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(fabsf(pa.x), fabsf(pa.y)),
+                                   fmaxf(fabsf(pa.z), fabsf(pa.w))),
+                             fmaxf(fmaxf(fabsf(pb.x), fabsf(pb.y)),
+                                   fmaxf(fabsf(pb.z), fabsf(pb.w)))));
+  }
+  for (int off = 32; off > 0; off >>= 1)
+    vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+  float *red = reinterpret_cast<float *>(lds + DegridMfmaLds::kWords - 8);
+  if (lane == 0) red[wave] = vmax;
+  __syncthreads();
+  vmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
+  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
+
+  float4 *geo_lds = reinterpret_cast<float4 *>(lds);
+  uint2 *bfr = reinterpret_cast<uint2 *>(lds + DegridMfmaLds::kGeoWords);
+
+  for (int t0 = 0; t0 < nt; t0 += 64) {  // 4 waves x 16 timesteps
+    const int t_row = t0 + wave * 16 + col;  // this lane's A row timestep
+    const idg::UVWCoordinate<float> c = uvw[g.time_offset + min(t_row, nt - 1)];
+    for (int cg0 = 0; cg0 < C; cg0 += CT) {
+      floatx4 acc[CT];
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[j] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+
+      for (int pc0 = 0; pc0 < half; pc0 += kPixChunk) {
+        const int cnt = min(kPixChunk, half - pc0);
+        __syncthreads();
+        for (int q = tid; q < kPixChunk; q += kBlock) {
+          const int ks = q >> 2, gq = q & 3;
+          if (q < cnt) {
+            const int b = pc0 + q;
+            float4 pa, pb, geo, ma, mb, mgeo;
+            pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
+                        aterms, sg, pa, pb, geo);
+            pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
+                        spheroidal, aterms, sg, ma, mb, mgeo);
+            geo_lds[q] = geo;
+            const float bv[8] = {pa.x, pa.y, pa.z, pa.w,
+                                 pb.x, pb.y, pb.z, pb.w};
+            const float mv[8] = {ma.x, ma.y, ma.z, ma.w,
+                                 mb.x, mb.y, mb.z, mb.w};
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) {
+              const int pol = (cc & 7) >> 1;
+              uint2 d;
+              d.x = p_coeff(bv[2 * pol] * scale, bv[2 * pol + 1] * scale, cc,
+                            false);
+              d.y = p_coeff(mv[2 * pol] * scale, mv[2 * pol + 1] * scale, cc,
+                            true);
+              bfr[ks * 64 + gq * 16 + cc] = d;
+            }
+          } else {
+            geo_lds[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc)
+              bfr[ks * 64 + gq * 16 + cc] = make_uint2(0u, 0u);
+          }
+        }
+        __syncthreads();
+        const int nks = (cnt + 3) / 4;
+        for (int ks = 0; ks < nks; ++ks) {
+          const float4 geo = geo_lds[4 * ks + grp];
+          const uint2 bb = bfr[ks * 64 + lane];
+          const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
+          // phase_index = fma(u, l, v*m) + w*n with w = 0
+          const float pidx = fma_(c.u, geo.x, c.v * geo.y);
+          for (int jb = 0; jb < CT; jb += CB) {
+            const float ka = wavenumbers[min(cg0 + jb, C - 1)];
+            const float A = fma_(pidx, ka, -geo.w);
+            const float R = revolutions(A);
+#pragma unroll
+            for (int j = jb; j < jb + CB && j < CT; ++j) {
+              const float k = wavenumbers[min(cg0 + j, C - 1)];
+              const float ph = fma_(pidx, k, -geo.w);
+              const float r = fma_(ph - A, kInv2PiHi, R);
+              float sn, cs;
+              sincos_rev(r, &sn, &cs);
+              unsigned hi, lo;
+              split_pair(cs, sn, &hi, &lo);
+              acc[j] = mfma16(pack4(hi, lo, hi, lo), bf, acc[j]);
+            }
+          }
+        }
+      }
+
+      // D rows = timesteps wave*16 + grp*4 + r, col = component (hi | lo).
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        const int ch = cg0 + j;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[j][r];
+          const float other = __shfl_xor(v, 8);
+          const int t = t0 + wave * 16 + grp * 4 + r;
+          if (col < 8 && t < nt && ch < C) {
+            float *dst = reinterpret_cast<float *>(
+                visibilities + ((g.time_offset + t) * C + ch) * 4);
+            dst[col] = (v + other) * unscale;
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
-template <int S_CT, int CG>
+// CG: channels per lane (VALU paths); IMPL: mirror path 0 = VALU, 1 = MFMA;
+// CT: channel tiles per MFMA pass.
+template <int S_CT, int CG, int IMPL, int CT>
 __global__ void __launch_bounds__(kBlock)
     kernel_degridder_mi355x(const int grid_size, int subgrid_size,
                             float image_size, float w_step_in_lambda,
@@ -97,8 +265,13 @@ __global__ void __launch_bounds__(kBlock)
   // general: [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l,m,n,poff)
   // mirror : [pair][0..1] = P'(base), [pair][2..3] = P'(mirror),
   //          [pair][4] = geometry of the base pixel
+  // One LDS allocation shared by all paths (the MFMA path aliases it).
   __shared__ float4 table[kChunk * 3];
   static_assert(kPairChunk * 5 <= kChunk * 3, "table size");
+  static_assert(DegridMfmaLds::kWords <= kChunk * 3 * 4, "mfma lds size");
+  // The VALU paths of an MFMA build are fallbacks (w != 0, odd S): they use
+  // 4 channels per lane to keep the kernel's register budget low.
+  constexpr int CGV = IMPL == 1 ? 4 : CG;
 
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
@@ -108,23 +281,37 @@ __global__ void __launch_bounds__(kBlock)
                                        w_step_in_lambda);
   const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const int C = nr_channels;
-  const int ncg = (C + CG - 1) / CG;
+  const int ncg = (C + CGV - 1) / CGV;
   const int nunits = g.nr_timesteps * ncg;
   const bool mirror_ok = (S % 2 == 0) && g.w_offset == 0.0f;
+
+  if (IMPL == 1 && mirror_ok) {
+    // Subgrid-uniform: w = 0 on every timestep.
+    bool w_nonzero = false;
+    for (int t = tid; t < g.nr_timesteps; t += kBlock)
+      w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+    if (__syncthreads_or(w_nonzero) == 0) {
+      degrid_mirror_mfma<S_CT, CT, 16>(g, S, npix, image_size, C, nr_stations,
+                                      uvw, wavenumbers, visibilities,
+                                      spheroidal, aterms, sg,
+                                      reinterpret_cast<unsigned *>(table));
+      return;
+    }
+  }
 
   for (int ubase = 0; ubase < nunits; ubase += kBlock) {
     const int unit = min(ubase + tid, nunits - 1);
     const bool active = ubase + tid < nunits;
     const int t = unit / ncg;
-    const int c0 = (unit - t * ncg) * CG;
+    const int c0 = (unit - t * ncg) * CGV;
     const long long row = g.time_offset + t;
     const idg::UVWCoordinate<float> c = uvw[row];
-    float k[CG];
+    float k[CGV];
 #pragma unroll
-    for (int j = 0; j < CG; ++j) k[j] = wavenumbers[min(c0 + j, C - 1)];
-    float acc[CG][8];
+    for (int j = 0; j < CGV; ++j) k[j] = wavenumbers[min(c0 + j, C - 1)];
+    float acc[CGV][8];
 #pragma unroll
-    for (int j = 0; j < CG; ++j)
+    for (int j = 0; j < CGV; ++j)
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[j][q] = 0.0f;
 
@@ -160,7 +347,7 @@ __global__ void __launch_bounds__(kBlock)
           const float A = fma_(pidx, k[0], -geo.w);
           const float R = revolutions(A);
 #pragma unroll
-          for (int j = 0; j < CG; ++j) {
+          for (int j = 0; j < CGV; ++j) {
             const float ph = fma_(pidx, k[j], -geo.w);
             const float r = fma_(ph - A, kInv2PiHi, R);
             float sn, cs;
@@ -188,7 +375,7 @@ __global__ void __launch_bounds__(kBlock)
           const float A = fma_(pidx, k[0], -geo.w);
           const float R = revolutions(A);
 #pragma unroll
-          for (int j = 0; j < CG; ++j) {
+          for (int j = 0; j < CGV; ++j) {
             const float ph = fma_(pidx, k[j], -geo.w);
             const float r = fma_(ph - A, kInv2PiHi, R);
             float sn, cs;
@@ -203,7 +390,7 @@ __global__ void __launch_bounds__(kBlock)
       float4 *dst = reinterpret_cast<float4 *>(
           visibilities + (row * C + c0) * 4);
 #pragma unroll
-      for (int j = 0; j < CG; ++j) {
+      for (int j = 0; j < CGV; ++j) {
         if (c0 + j < C) {
           dst[2 * j] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
           dst[2 * j + 1] =
@@ -214,25 +401,37 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-#define IDG_DEGRIDDER(S_, CG_) \
-  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_>)
+#define IDG_DEGRIDDER(S_, CG_, IMPL_) \
+  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_, IMPL_, 16>)
+
+// IDG_DEGRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
+static int degridder_impl() {
+  const char *v = std::getenv("IDG_DEGRIDDER_IMPL");
+  return (v && std::string(v) == "valu") ? 0 : 1;
+}
 
 KernelChoice select_degridder(const Problem &p) {
   KernelChoice k;
   k.grid = p.nr_subgrids;
   k.block = kBlock;
   const int C = p.nr_channels;
-  const int cg = C % 8 == 0 ? 8 : (C % 4 == 0 ? 4 : (C >= 8 ? 8 : 4));
+  const bool cg8 = C % 8 == 0 || (C % 4 != 0 && C >= 8);
   const bool s32 = p.subgrid_size == 32, s64 = p.subgrid_size == 64;
-  if (cg == 8) {
-    k.func = s32 ? IDG_DEGRIDDER(32, 8)
-                 : (s64 ? IDG_DEGRIDDER(64, 8) : IDG_DEGRIDDER(0, 8));
-  } else {
-    k.func = s32 ? IDG_DEGRIDDER(32, 4)
-                 : (s64 ? IDG_DEGRIDDER(64, 4) : IDG_DEGRIDDER(0, 4));
-  }
-  k.name = s32 ? "degridder_mi355x_s32"
-               : (s64 ? "degridder_mi355x_s64" : "degridder_mi355x_generic");
+  const bool mfma = degridder_impl() == 1;
+#define IDG_PICK(CG_)                                                      \
+  (mfma ? (s32 ? IDG_DEGRIDDER(32, CG_, 1)                                 \
+               : (s64 ? IDG_DEGRIDDER(64, CG_, 1) : IDG_DEGRIDDER(0, CG_, 1))) \
+        : (s32 ? IDG_DEGRIDDER(32, CG_, 0)                                 \
+               : (s64 ? IDG_DEGRIDDER(64, CG_, 0) : IDG_DEGRIDDER(0, CG_, 0))))
+  k.func = cg8 ? IDG_PICK(8) : IDG_PICK(4);
+#undef IDG_PICK
+  if (mfma)
+    k.name = s32 ? "degridder_mi355x_s32"
+                 : (s64 ? "degridder_mi355x_s64" : "degridder_mi355x_generic");
+  else
+    k.name = s32 ? "degridder_mi355x_s32_valu"
+                 : (s64 ? "degridder_mi355x_s64_valu"
+                        : "degridder_mi355x_generic_valu");
   return k;
 }
 

@@ -331,6 +331,12 @@ __device__ __forceinline__ void grid_mirror_mfma(
                 accb[i] = mfma16(af, bf, accb[i]);
                 accm[i] = mfma16(af, bm, accm[i]);
               }
+              // Keep each channel pair's MFMAs inside its own iteration.  When
+              // the scheduler sinks all eight MFMAs to the end of the loop
+              // body, the last tile's accumulators come out corrupted (a
+              // few % of subgrids, run-to-run different, only with >1 wave
+              // per SIMD; tests/debug/diff_detail.py).
+              __builtin_amdgcn_sched_barrier(0);
             }
           }
         }

@@ -8,7 +8,10 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libidg_mi355x.so")
+# IDG_MI355X_LIB selects another build of the same library (A/B-testing a
+# kernel variant); it is read once, at import.
+LIB_PATH = os.environ.get("IDG_MI355X_LIB") or os.path.join(
+    PKG_DIR, "libidg_mi355x.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
