@@ -1,0 +1,16 @@
+#!/bin/bash
+# Profiles the default bench workload on the GPU box: kernel trace + stats,
+# then FETCH_SIZE and WRITE_SIZE in separate PMC passes (never combined with
+# trace domains).  Output under gpurun_out/prof_<tag>/.
+set -eo pipefail
+tag=${1:-r01}
+out=$GRAFT_REPO_ROOT/gpurun_out/prof_$tag
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ktrace" -o run -- \
+  python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$out/bench_ktrace.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
+  python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
+  python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
+echo done
