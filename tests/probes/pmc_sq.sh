@@ -1,0 +1,19 @@
+#!/bin/bash
+# SQ instruction-mix / busy counters for the bench workload, one pass per
+# group (gfx950 block limits).  Output under gpurun_out/pmc_<tag>/.
+set -eo pipefail
+tag=${1:-sq}
+out=$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+rocprofv3 -L > "$out/avail.txt" 2>&1 || true
+i=0
+for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
+           "SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU_MFMA_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY" \
+           "SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || echo "pass $i failed"
+done
+echo done
