@@ -175,41 +175,45 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 // ---------------------------------------------------------------------------
 // MFMA mirror path (even S, w = 0 on every timestep, w_offset = 0).
 //
-// GEMM per 16-pixel tile: O[pixel][col] += sum_k A[pixel][k] * B[k][col],
-//   k = 8 items x {cos_hi, sin_hi, cos_lo, sin_lo}   (v_mfma_f32_16x16x32_f16)
-//   A = phasors of the BASE pixels (VALU: exact phase, revolutions, v_sin /
-//       v_cos, split into f16 hi/lo), B = visibility coefficients (cos row:
-//       V.re | V.im, sin row: -V.im | V.re) with columns [8 hi | 8 lo],
-//   the MIRROR tile reuses A with the sin rows of B negated.
-// Lane l = (group g = l/16, column/pixel l%16).  Lane group g takes timestep
-// t = 4q + g of each timestep quad q, so every lane keeps its own
-// phase_index / anchor in registers and shares nothing across lanes.
-// B fragments of KS_BUF K-steps are built once per workgroup in LDS.
+// For a base pixel with phasor (c, s) = exp(i*phase) and its mirror (phase
+// exactly negated), the contribution of a visibility V is
+//   base   += X + Y,   mirror += X - Y,   X = c * Bc,  Y = s * Bs,
+// with Bc = (V.re | V.im) and Bs = (-V.im | V.re) per correlation.  X and Y
+// are two dense GEMMs per 16-pixel tile (v_mfma_f32_16x16x32_f16):
+//   X[pixel][col] += sum_k Ac[pixel][k] * Bc[k][col]      (Y likewise)
+// K = 16 items (4 timesteps x 4 channels) x {hi, lo} of the f16-split phasor
+// component; B columns = 8 components [hi | lo] of the f16-split visibility.
+// Lane l = (group g = l/16, pixel/column l%16): group g takes timestep 4q+g of
+// timestep quad q and 4 consecutive channels, so the lane's K-block is
+//   [cA_h, cB_h, cA_l, cB_l, cC_h, cD_h, cC_l, cD_l]
+// (split_pair on channel pairs: one v_cvt_pk + two v_fma_mix per pair) and
+// B's rows for it are (bcA, bcB, bcA, bcB, bcC, bcD, bcC, bcD): 4 dwords
+// (x, x, y, y) per lane, stored pre-expanded in LDS.  Per phasor: 1.5 packed
+// phase instructions, v_sin + v_cos, 3 split instructions, half an MFMA.
 // ---------------------------------------------------------------------------
-constexpr int kKsBuf = 32;               // K-steps of B fragments per fill
-constexpr unsigned kNegHi = 0x80000000u;  // negates the sin-row f16
+constexpr int kKsBuf = 16;  // K-steps (16 items each) of B fragments per fill
 
 template <int PT>
 struct MfmaLds {
-  static constexpr int kObufFloats = 2 * 64 * PT * 16;
-  static constexpr int kBbufWords = kKsBuf * 64 * 2;
+  static constexpr int kObufFloats = 2 * 64 * PT * 16;  // X and Y tiles
+  static constexpr int kBbufWords = kKsBuf * 64 * 8;    // uint4 X + uint4 Y
   static constexpr int kWords =
       (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
 };
 
-// f16 coefficient dword (cos-row, sin-row) of one visibility item for the
-// B column `col` of the lane, pre-scaled by `scale` (a power of two).
-__device__ __forceinline__ unsigned b_coeff(const float2 *__restrict__ vis,
-                                            long long item, int col,
-                                            float scale) {
-  const int pol = (col & 7) >> 1;
-  const float2 v = vis[item * 4 + pol];
+// (Bc, Bs) of one visibility item for B column `col`, pre-scaled.  `vis`
+// points at the subgrid's first visibility row; `item` = t * C + c.
+__device__ __forceinline__ float2 b_pair(const float2 *__restrict__ vis,
+                                         int item, int col, float scale) {
+  const float2 v = vis[item * 4 + ((col & 7) >> 1)];
   const float re = v.x * scale, im = v.y * scale;
-  const bool imag_col = col & 1;
-  const float bc = imag_col ? im : re;
-  const float bs = imag_col ? re : -im;
+  return (col & 1) ? make_float2(im, re) : make_float2(re, -im);
+}
+
+// hi (col < 8) or lo (col >= 8) f16 parts of (a, b) packed into one dword.
+__device__ __forceinline__ unsigned b_half(float a, float b, int col) {
   unsigned hi, lo;
-  split_pair(bc, bs, &hi, &lo);
+  split_pair(a, b, &hi, &lo);
   return (col & 8) ? lo : hi;
 }
 
@@ -221,12 +225,13 @@ __device__ __forceinline__ void grid_mirror_mfma(
     const float2 *__restrict__ visibilities,
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
     float2 *__restrict__ out, unsigned *lds) {
+  static_assert(CB % 4 == 0, "anchor blocks hold whole channel quads");
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
   const int half = npix / 2;
   const int nt = g.nr_timesteps;
-  const int npairs = (C + 1) / 2;
+  const int nchq = (C + 3) / 4;  // channel quads
 
   // Per-subgrid power-of-two scale keeps every visibility inside f16 range.
   float vmax = 0.0f;
@@ -250,92 +255,131 @@ __device__ __forceinline__ void grid_mirror_mfma(
   if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
   const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
 
-  const float2 *vsub = visibilities;  // indexed by absolute item below
-  uint2 *bbuf = reinterpret_cast<uint2 *>(lds);
+  const float2 *__restrict__ vsub = visibilities + g.time_offset * C * 4;
+  uint4 *bbuf = reinterpret_cast<uint4 *>(lds);  // [ks][64][X, Y]
   float *obuf = reinterpret_cast<float *>(lds);
   const int nquads = (nt + 3) / 4;
-  const int quads_per_fill = npairs <= kKsBuf ? kKsBuf / npairs : 1;
+  const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
+  const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
 
   for (int gbase = 0; gbase < half; gbase += 64 * PT) {
-    float lg[PT], mg[PT], pg[PT];
+    float lg[PT], mg[PT];
+    floatx2 pg2[PT];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
-      float n_unused;
-      pixel_geometry(b, S, image_size, g, lg[i], mg[i], n_unused, pg[i]);
+      float n_unused, pg;
+      pixel_geometry(b, S, image_size, g, lg[i], mg[i], n_unused, pg);
+      pg2[i] = floatx2{pg, pg};
     }
-    floatx4 accb[PT], accm[PT];
+    floatx4 accx[PT], accy[PT];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      accb[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-      accm[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+      accx[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+      accy[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
     }
 
     for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
       const int nq = min(quads_per_fill, nquads - q0);
-      for (int p0 = 0; p0 < npairs; p0 += kKsBuf) {
-        const int np = min(kKsBuf, npairs - p0);
-        // ---- B fragments for nq quads x np channel pairs -> LDS ----
+      for (int j0 = 0; j0 < nchq; j0 += cq_per_fill) {
+        const int nj = min(cq_per_fill, nchq - j0);
+        // ---- B fragments for nq timestep quads x nj channel quads -> LDS
         __syncthreads();
-        for (int w = tid; w < nq * np * 64; w += kBlock) {
+        for (int w = tid; w < nq * nj * 64; w += kBlock) {
           const int lw = w & 63, ks = w >> 6;
-          const int qq = ks / np, jj = ks - qq * np;
+          const int qq = ks / nj, jj = ks - qq * nj;
           const int t = (q0 + qq) * 4 + (lw >> 4);
-          const int c0 = 2 * (p0 + jj);
-          uint2 d = make_uint2(0u, 0u);
-          if (t < nt) {
-            const long long item = (g.time_offset + t) * C + c0;
-            d.x = b_coeff(vsub, item, lw & 15, scale);
-            if (c0 + 1 < C) d.y = b_coeff(vsub, item + 1, lw & 15, scale);
+          const int c0 = 4 * (j0 + jj);
+          const int cl = lw & 15;
+          float2 b[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            b[u] = make_float2(0.0f, 0.0f);
+            if (t < nt && c0 + u < C)
+              b[u] = b_pair(vsub, t * C + c0 + u, cl, scale);
           }
-          bbuf[ks * 64 + lw] = d;
+          const unsigned xc = b_half(b[0].x, b[1].x, cl);
+          const unsigned yc = b_half(b[2].x, b[3].x, cl);
+          const unsigned xs = b_half(b[0].y, b[1].y, cl);
+          const unsigned ys = b_half(b[2].y, b[3].y, cl);
+          bbuf[(ks * 64 + lw) * 2] = make_uint4(xc, xc, yc, yc);
+          bbuf[(ks * 64 + lw) * 2 + 1] = make_uint4(xs, xs, ys, ys);
         }
         __syncthreads();
         // ---- MFMA over the buffered K-steps ----
         for (int qq = 0; qq < nq; ++qq) {
           const int t = min((q0 + qq) * 4 + grp, nt - 1);
           const idg::UVWCoordinate<float> c = uvw[g.time_offset + t];
-          float pidx[PT], A[PT], R[PT];
+          floatx2 np2[PT];
 #pragma unroll
-          for (int i = 0; i < PT; ++i) pidx[i] = fma_(c.u, lg[i], c.v * mg[i]);
-          // channel blocks of CB channels share one phase anchor
-          for (int jb = 0; jb < np; jb += CB / 2) {
-            const int je = min(jb + CB / 2, np);
-            const float ka = wavenumbers[2 * (p0 + jb)];
+          for (int i = 0; i < PT; ++i) {
+            const float pidx = fma_(c.u, lg[i], c.v * mg[i]);
+            np2[i] = floatx2{-pidx, -pidx};
+          }
+          for (int jb = 0; jb < nj; jb += CB / 4) {
+            const int je = min(jb + CB / 4, nj);
+            // anchor: phase at the block's first channel
+            const float ka = wavenumbers[4 * (j0 + jb)];
+            floatx2 A2[PT], R2[PT];
+            static_assert(PT % 2 == 0, "anchors are formed for tile pairs");
 #pragma unroll
-            for (int i = 0; i < PT; ++i) {
-              A[i] = fma_(-pidx[i], ka, pg[i]);
-              R[i] = revolutions(A[i]);
+            for (int i = 0; i < PT; i += 2) {
+              // revolutions() of two tiles' anchors in packed arithmetic
+              const floatx2 a = __builtin_elementwise_fma(
+                  floatx2{np2[i].x, np2[i + 1].x}, floatx2{ka, ka},
+                  floatx2{pg2[i].x, pg2[i + 1].x});
+              const floatx2 ih = {kInv2PiHi, kInv2PiHi};
+              const floatx2 hi = a * ih;
+              floatx2 lo = __builtin_elementwise_fma(a, ih, -hi);
+              lo = __builtin_elementwise_fma(
+                  a, floatx2{kInv2PiLo, kInv2PiLo}, lo);
+              const floatx2 rn = {__builtin_rintf(hi.x), __builtin_rintf(hi.y)};
+              const floatx2 r = (hi - rn) + lo;
+              A2[i] = floatx2{a.x, a.x};
+              A2[i + 1] = floatx2{a.y, a.y};
+              R2[i] = floatx2{r.x, r.x};
+              R2[i + 1] = floatx2{r.y, r.y};
             }
             for (int jj = jb; jj < je; ++jj) {
-              const int c0 = 2 * (p0 + jj);
-              const float k0 = wavenumbers[c0];
-              const float k1 = wavenumbers[min(c0 + 1, C - 1)];
-              const uint2 bb = bbuf[(qq * np + jj) * 64 + lane];
-              const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
-              const half8 bm = pack4(bb.x ^ kNegHi, bb.x ^ kNegHi,
-                                     bb.y ^ kNegHi, bb.y ^ kNegHi);
+              const int c0 = 4 * (j0 + jj);
+              const floatx2 k01 = {wavenumbers[min(c0, C - 1)],
+                                   wavenumbers[min(c0 + 1, C - 1)]};
+              const floatx2 k23 = {wavenumbers[min(c0 + 2, C - 1)],
+                                   wavenumbers[min(c0 + 3, C - 1)]};
+              const int ks = qq * nj + jj;
+              const uint4 bx = bbuf[(ks * 64 + lane) * 2];
+              const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
+              const half8 bfx = pack4(bx.x, bx.y, bx.z, bx.w);
+              const half8 bfy = pack4(by.x, by.y, by.z, by.w);
+              const floatx2 inv2pi = {kInv2PiHi, kInv2PiHi};
 #pragma unroll
               for (int i = 0; i < PT; ++i) {
-                const float ph0 = fma_(-pidx[i], k0, pg[i]);
-                const float ph1 = fma_(-pidx[i], k1, pg[i]);
-                const float r0 = fma_(ph0 - A[i], kInv2PiHi, R[i]);
-                const float r1 = fma_(ph1 - A[i], kInv2PiHi, R[i]);
-                float s0, c0f, s1, c1f;
-                sincos_rev(r0, &s0, &c0f);
-                sincos_rev(r1, &s1, &c1f);
-                unsigned h0, l0, h1, l1;
-                split_pair(c0f, s0, &h0, &l0);
-                split_pair(c1f, s1, &h1, &l1);
-                const half8 af = pack4(h0, l0, h1, l1);
-                accb[i] = mfma16(af, bf, accb[i]);
-                accm[i] = mfma16(af, bm, accm[i]);
+                const floatx2 p01 = __builtin_elementwise_fma(np2[i], k01,
+                                                              pg2[i]);
+                const floatx2 p23 = __builtin_elementwise_fma(np2[i], k23,
+                                                              pg2[i]);
+                const floatx2 r01 =
+                    __builtin_elementwise_fma(p01 - A2[i], inv2pi, R2[i]);
+                const floatx2 r23 =
+                    __builtin_elementwise_fma(p23 - A2[i], inv2pi, R2[i]);
+                float s0, c0f, s1, c1f, s2, c2f, s3, c3f;
+                sincos_rev(r01.x, &s0, &c0f);
+                sincos_rev(r01.y, &s1, &c1f);
+                sincos_rev(r23.x, &s2, &c2f);
+                sincos_rev(r23.y, &s3, &c3f);
+                unsigned hc01, lc01, hc23, lc23, hs01, ls01, hs23, ls23;
+                split_pair(c0f, c1f, &hc01, &lc01);
+                split_pair(c2f, c3f, &hc23, &lc23);
+                split_pair(s0, s1, &hs01, &ls01);
+                split_pair(s2, s3, &hs23, &ls23);
+                accx[i] = mfma16(pack4(hc01, lc01, hc23, lc23), bfx, accx[i]);
+                accy[i] = mfma16(pack4(hs01, ls01, hs23, ls23), bfy, accy[i]);
               }
-              // Keep each channel pair's MFMAs inside its own iteration.  When
-              // the scheduler sinks all eight MFMAs to the end of the loop
-              // body, the last tile's accumulators come out corrupted (a
-              // few % of subgrids, run-to-run different, only with >1 wave
-              // per SIMD; tests/debug/diff_detail.py).
+              // Keep each K-step's MFMAs inside its own iteration.  When the
+              // scheduler sank all of an iteration's MFMAs to the end of the
+              // loop body, the last tile's accumulators came out corrupted
+              // (a few % of subgrids, run-to-run different, only with >1
+              // wave per SIMD; DESIGN.md §4.4, tests/debug/diff_detail.py).
               __builtin_amdgcn_sched_barrier(0);
             }
           }
@@ -343,29 +387,41 @@ __device__ __forceinline__ void grid_mirror_mfma(
       }
     }
 
-    // ---- epilogue: D tiles -> LDS [pixel][16], hi + lo, A-term, store ----
+    // ---- epilogue: X, Y tiles -> LDS [pixel][16]; base = X + Y, mirror =
+    // X - Y; hi + lo; A-term; store ----
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PT; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int lp = (wave * PT + i) * 16 + grp * 4 + r;
-        obuf[lp * 16 + col] = accb[i][r];
-        obuf[(64 * PT + lp) * 16 + col] = accm[i][r];
+        obuf[lp * 16 + col] = accx[i][r];
+        obuf[(64 * PT + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
-    for (int q = tid; q < 2 * 64 * PT; q += kBlock) {
-      const bool mir = q >= 64 * PT;
-      const int b = gbase + (mir ? q - 64 * PT : q);
+    for (int q = tid; q < 64 * PT; q += kBlock) {
+      const int b = gbase + q;
       if (b >= half) continue;
-      const float4 *o4 = reinterpret_cast<const float4 *>(obuf + q * 16);
-      const float4 h0 = o4[0], h1 = o4[1], l0 = o4[2], l1 = o4[3];
-      float a[8] = {(h0.x + l0.x) * unscale, (h0.y + l0.y) * unscale,
-                    (h0.z + l0.z) * unscale, (h0.w + l0.w) * unscale,
-                    (h1.x + l1.x) * unscale, (h1.y + l1.y) * unscale,
-                    (h1.z + l1.z) * unscale, (h1.w + l1.w) * unscale};
-      store_pixel(a, mir ? npix - 1 - b : b, S, npix, g, nr_stations,
-                  spheroidal, aterms, out);
+      const float4 *xr = reinterpret_cast<const float4 *>(obuf + q * 16);
+      const float4 *yr =
+          reinterpret_cast<const float4 *>(obuf + (64 * PT + q) * 16);
+      const float4 xh0 = xr[0], xh1 = xr[1], xl0 = xr[2], xl1 = xr[3];
+      const float4 yh0 = yr[0], yh1 = yr[1], yl0 = yr[2], yl1 = yr[3];
+      const float x[8] = {xh0.x + xl0.x, xh0.y + xl0.y, xh0.z + xl0.z,
+                          xh0.w + xl0.w, xh1.x + xl1.x, xh1.y + xl1.y,
+                          xh1.z + xl1.z, xh1.w + xl1.w};
+      const float y[8] = {yh0.x + yl0.x, yh0.y + yl0.y, yh0.z + yl0.z,
+                          yh0.w + yl0.w, yh1.x + yl1.x, yh1.y + yl1.y,
+                          yh1.z + yl1.z, yh1.w + yl1.w};
+      float ab[8], am[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ab[j] = (x[j] + y[j]) * unscale;
+        am[j] = (x[j] - y[j]) * unscale;
+      }
+      store_pixel(ab, b, S, npix, g, nr_stations, spheroidal, aterms, out);
+      store_pixel(am, npix - 1 - b, S, npix, g, nr_stations, spheroidal,
+                  aterms, out);
     }
     __syncthreads();
   }
@@ -378,7 +434,7 @@ __device__ __forceinline__ void grid_mirror_mfma(
 // IMPL: mirror-path implementation, 0 = VALU (v_pk_fma MAC), 1 = MFMA.
 // PT  : 16-pixel base tiles per wave in the MFMA path.
 template <int S_CT, int PPT, int CB, int IMPL, int PT>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock, 4)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
                           float image_size, float w_step_in_lambda,
                           int nr_channels, int nr_stations,
