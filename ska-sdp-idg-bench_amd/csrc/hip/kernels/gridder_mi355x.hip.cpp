@@ -37,6 +37,14 @@
 #include "lib-hip.hpp"
 #include "mfma.hpp"
 
+// MFMA tiles per wave and the waves-per-SIMD launch bound (tuning knobs).
+#ifndef IDG_GRID_PT
+#define IDG_GRID_PT 4
+#endif
+#ifndef IDG_GRID_WAVES
+#define IDG_GRID_WAVES 4
+#endif
+
 namespace idg_mi355x {
 
 namespace {
@@ -201,22 +209,6 @@ struct MfmaLds {
       (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
 };
 
-// (Bc, Bs) of one visibility item for B column `col`, pre-scaled.  `vis`
-// points at the subgrid's first visibility row; `item` = t * C + c.
-__device__ __forceinline__ float2 b_pair(const float2 *__restrict__ vis,
-                                         int item, int col, float scale) {
-  const float2 v = vis[item * 4 + ((col & 7) >> 1)];
-  const float re = v.x * scale, im = v.y * scale;
-  return (col & 1) ? make_float2(im, re) : make_float2(re, -im);
-}
-
-// hi (col < 8) or lo (col >= 8) f16 parts of (a, b) packed into one dword.
-__device__ __forceinline__ unsigned b_half(float a, float b, int col) {
-  unsigned hi, lo;
-  split_pair(a, b, &hi, &lo);
-  return (col & 8) ? lo : hi;
-}
-
 template <int S_CT, int PT, int CB>
 __device__ __forceinline__ void grid_mirror_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
@@ -256,6 +248,7 @@ __device__ __forceinline__ void grid_mirror_mfma(
   const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
 
   const float2 *__restrict__ vsub = visibilities + g.time_offset * C * 4;
+
   uint4 *bbuf = reinterpret_cast<uint4 *>(lds);  // [ks][64][X, Y]
   float *obuf = reinterpret_cast<float *>(lds);
   const int nquads = (nt + 3) / 4;
@@ -283,27 +276,53 @@ __device__ __forceinline__ void grid_mirror_mfma(
       const int nq = min(quads_per_fill, nquads - q0);
       for (int j0 = 0; j0 < nchq; j0 += cq_per_fill) {
         const int nj = min(cq_per_fill, nchq - j0);
-        // ---- B fragments for nq timestep quads x nj channel quads -> LDS
+        // ---- B fragments for nq timestep quads x nj channel quads -> LDS.
+        // One wave fills one K-step (lane = group g, column col): items
+        // (t = 4q+g, c0..c0+3), each a float2 load of the column's
+        // correlation; bc/bs formed with the lane's (re, im) selectors,
+        // then split to the column's f16 part.
         __syncthreads();
-        for (int w = tid; w < nq * nj * 64; w += kBlock) {
-          const int lw = w & 63, ks = w >> 6;
-          const int qq = ks / nj, jj = ks - qq * nj;
-          const int t = (q0 + qq) * 4 + (lw >> 4);
-          const int c0 = 4 * (j0 + jj);
-          const int cl = lw & 15;
-          float2 b[4];
+        {
+          // this lane's B column: correlation, (re | im) selectors with the
+          // scale folded in, and which f16 part (hi: 0, lo: -1) it holds
+          const int bpol = (col & 7) >> 1;
+          const float sel_re = (col & 1) ? 0.0f : scale;
+          const float sel_im = (col & 1) ? scale : 0.0f;
+          const float bpart = (col & 8) ? -1.0f : 0.0f;
+          const int nks = nq * nj;
+          const bool full = (q0 + nq) * 4 <= nt && 4 * (j0 + nj) <= C;
+          for (int ks = wave; ks < nks; ks += kBlock / 64) {
+            const int qq = ks / nj, jj = ks - qq * nj;
+            const int t = (q0 + qq) * 4 + grp;
+            const int c0 = 4 * (j0 + jj);
+            float2 b[4];
+            if (full) {
+              const float2 *src = vsub + (t * C + c0) * 4 + bpol;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            b[u] = make_float2(0.0f, 0.0f);
-            if (t < nt && c0 + u < C)
-              b[u] = b_pair(vsub, t * C + c0 + u, cl, scale);
+              for (int u = 0; u < 4; ++u) b[u] = src[4 * u];
+            } else {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const bool ok = t < nt && c0 + u < C;
+                const int it = ok ? t * C + c0 + u : 0;
+                const float2 v = vsub[it * 4 + bpol];
+                b[u] = ok ? v : make_float2(0.0f, 0.0f);
+              }
+            }
+            float bc[4], bs[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              // column (re): bc = re, bs = -im;  column (im): bc = im, bs = re
+              bc[u] = fma_(b[u].y, sel_im, b[u].x * sel_re);
+              bs[u] = fma_(b[u].x, sel_im, -(b[u].y * sel_re));
+            }
+            const unsigned xc = split_part(bc[0], bc[1], bpart);
+            const unsigned yc = split_part(bc[2], bc[3], bpart);
+            const unsigned xs = split_part(bs[0], bs[1], bpart);
+            const unsigned ys = split_part(bs[2], bs[3], bpart);
+            bbuf[(ks * 64 + lane) * 2] = make_uint4(xc, xc, yc, yc);
+            bbuf[(ks * 64 + lane) * 2 + 1] = make_uint4(xs, xs, ys, ys);
           }
-          const unsigned xc = b_half(b[0].x, b[1].x, cl);
-          const unsigned yc = b_half(b[2].x, b[3].x, cl);
-          const unsigned xs = b_half(b[0].y, b[1].y, cl);
-          const unsigned ys = b_half(b[2].y, b[3].y, cl);
-          bbuf[(ks * 64 + lw) * 2] = make_uint4(xc, xc, yc, yc);
-          bbuf[(ks * 64 + lw) * 2 + 1] = make_uint4(xs, xs, ys, ys);
         }
         __syncthreads();
         // ---- MFMA over the buffered K-steps ----
@@ -399,6 +418,9 @@ __device__ __forceinline__ void grid_mirror_mfma(
         obuf[(64 * PT + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
+#ifdef IDG_DBG_NOEPI
+    if (gbase >= 0) { __syncthreads(); continue; }
+#endif
     for (int q = tid; q < 64 * PT; q += kBlock) {
       const int b = gbase + q;
       if (b >= half) continue;
@@ -434,7 +456,7 @@ __device__ __forceinline__ void grid_mirror_mfma(
 // IMPL: mirror-path implementation, 0 = VALU (v_pk_fma MAC), 1 = MFMA.
 // PT  : 16-pixel base tiles per wave in the MFMA path.
 template <int S_CT, int PPT, int CB, int IMPL, int PT>
-__global__ void __launch_bounds__(kBlock, 4)
+__global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
                           float image_size, float w_step_in_lambda,
                           int nr_channels, int nr_stations,
@@ -539,7 +561,7 @@ __global__ void __launch_bounds__(kBlock, 4)
 
 #define IDG_GRIDDER(S_, PPT_, IMPL_)                                     \
   reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mi355x<S_, PPT_, 16, IMPL_, 4>)
+      &kernel_gridder_mi355x<S_, PPT_, 16, IMPL_, IDG_GRID_PT>)
 
 // IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int gridder_impl() {

@@ -51,6 +51,25 @@ __device__ __forceinline__ void split_pair(float c, float s, unsigned *hi,
   *lo = lu;
 }
 
+// One f16 part of each of (a, b), packed: the hi part f16(x) where
+// m = 0, the lo part f16(x - f16(x)) where m = -1 (m is per lane, so lanes
+// holding B's hi columns and lanes holding its lo columns run the same
+// three instructions).
+__device__ __forceinline__ unsigned split_part(float a, float b, float m) {
+  floatx2 v = {a, b};
+  const unsigned hu =
+      __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
+  unsigned r;
+  asm volatile("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]"
+               : "=&v"(r)
+               : "v"(hu), "v"(m), "v"(a));
+  asm volatile("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] "
+               "op_sel_hi:[1,0,0]"
+               : "+v"(r)
+               : "v"(hu), "v"(m), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ floatx4 mfma16(const half8 &a, const half8 &b,
                                           const floatx4 &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
