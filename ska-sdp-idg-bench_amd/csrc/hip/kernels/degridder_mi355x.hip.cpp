@@ -35,6 +35,11 @@
 #include "lib-hip.hpp"
 #include "mfma.hpp"
 
+// waves-per-SIMD launch bound of the MFMA degridder (tuning knob)
+#ifndef IDG_DEGRID_WAVES
+#define IDG_DEGRID_WAVES 2
+#endif
+
 namespace idg_mi355x {
 
 constexpr int kChunk = 1024;  // general path: pixels per LDS table chunk
@@ -88,52 +93,48 @@ __device__ __forceinline__ void pixel_entry(
 // ---------------------------------------------------------------------------
 // MFMA mirror path (even S, w = 0 for every timestep, w_offset = 0).
 //
-// GEMM over pixels: O[item][col] += sum_k A[item][k] * B[k][col] with
-//   rows  = 16 timesteps of one channel (an item tile; CT tiles = CT
-//           channels share each lane's phase_index),
-//   k     = 4 base pixels (one per lane group) x {base, mirror} x
-//           {cos_hi, sin_hi, cos_lo, sin_lo}       (v_mfma_f32_16x16x32_f16)
-//   A     = phasors exp(i*phase(t, c, base pixel)) (VALU, exact phases),
-//           the mirror slot reuses them (phase(mirror) = -phase(base)),
-//   B     = P' coefficients (cos row: P.re | P.im, sin row: -P.im | P.re),
-//           mirror slot with its sin rows negated, columns [8 hi | 8 lo].
-// B fragments and pixel geometry of kPixChunk base pixels live in LDS.
+// A base pixel b and its mirror m have exactly negated phases, so their
+// contribution to a visibility is
+//   P'_b e^{i phi} + P'_m e^{-i phi} = cos(phi) * S + i sin(phi) * D,
+//   S = P'_b + P'_m,  D = P'_b - P'_m,
+// a real GEMM per channel over pixel pairs:
+//   O[t][col] += sum_k A[t][k] * B[k][col]             (v_mfma_f32_16x16x32_f16)
+//   A rows = 16 timesteps (lane l%16), K-block of lane group g = 2 pixel
+//   pairs (p0, p1) as [c0_h, c1_h, c0_l, c1_l, s0_h, s1_h, s0_l, s1_l],
+//   B rows = (Bc0, Bc1, Bc0, Bc1, Bs0, Bs1, Bs0, Bs1) with cos row
+//   Bc = (S.re | S.im) and sin row Bs = (-D.im | D.re) per correlation,
+//   columns [8 components hi | 8 lo] of the f16 split.
+// B does not depend on the timestep or channel: its fragments -- 2 dwords
+// (x = Bc pair, y = Bs pair) per lane per K-step of 8 pairs -- and the pair
+// geometry are built ONCE per chunk of KP pairs (the whole subgrid when
+// npix/2 <= KP) and reused by every timestep block and channel tile.
+// Per phasor: 1.5 packed phase instructions, v_sin + v_cos, 3 split
+// instructions, half an MFMA.
 // ---------------------------------------------------------------------------
-constexpr int kPixChunk = 256;  // base pixels per LDS chunk (64 K-steps)
-constexpr unsigned kNegHi = 0x80000000u;
-
+template <int KP>
 struct DegridMfmaLds {
-  static constexpr int kGeoWords = kPixChunk * 4;            // float4 each
-  static constexpr int kBfrWords = (kPixChunk / 4) * 64 * 2;  // uint2 each
+  static constexpr int kGeoWords = KP * 4;              // float4 per pair
+  static constexpr int kBfrWords = (KP / 8) * 64 * 2;   // uint2 per lane
   static constexpr int kWords = kGeoWords + kBfrWords + 8;
 };
 
-// (cos-row, sin-row) f16 coefficient dword of complex p for column col.
-__device__ __forceinline__ unsigned p_coeff(float re, float im, int col,
-                                            bool negate_sin) {
-  const bool imag_col = col & 1;
-  const float bc = imag_col ? im : re;
-  float bs = imag_col ? re : -im;
-  if (negate_sin) bs = -bs;
-  unsigned hi, lo;
-  split_pair(bc, bs, &hi, &lo);
-  return (col & 8) ? lo : hi;
-}
-
-template <int S_CT, int CT, int CB>
+template <int S_CT, int CT, int CB, int KP>
 __device__ __forceinline__ void degrid_mirror_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
     const float *__restrict__ wavenumbers, float2 *__restrict__ visibilities,
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
     const float2 *__restrict__ sg, unsigned *lds) {
+  static_assert(CT % CB == 0, "channel tiles hold whole anchor blocks");
+  static_assert(KP % 32 == 0, "chunks hold whole K-steps for 4 waves");
+  using L = DegridMfmaLds<KP>;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
   const int half = npix / 2;
   const int nt = g.nr_timesteps;
 
-  // Per-subgrid power-of-two scale of P' (f16 range).
+  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range.
   float vmax = 0.0f;
   for (int p = tid; p < npix; p += kBlock) {
     float4 pa, pb, geo;
@@ -146,83 +147,124 @@ __device__ __forceinline__ void degrid_mirror_mfma(
   }
   for (int off = 32; off > 0; off >>= 1)
     vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-  float *red = reinterpret_cast<float *>(lds + DegridMfmaLds::kWords - 8);
+  float *red = reinterpret_cast<float *>(lds + L::kWords - 8);
   if (lane == 0) red[wave] = vmax;
   __syncthreads();
-  vmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  vmax = 2.0f * fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   int e = 0;
   if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
   const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
 
   float4 *geo_lds = reinterpret_cast<float4 *>(lds);
-  uint2 *bfr = reinterpret_cast<uint2 *>(lds + DegridMfmaLds::kGeoWords);
+  uint2 *bfr = reinterpret_cast<uint2 *>(lds + L::kGeoWords);
+  const bool single = half <= KP;
 
+  // B fragments and geometry of pairs [pc0, pc0 + KP): one thread per
+  // K-block (2 pairs), writing all 16 column lanes of it.
+  auto build = [&](int pc0) {
+    for (int q = tid; q < KP / 2; q += kBlock) {
+      float sre[2][4], sim[2][4], dre[2][4], dim[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int b = pc0 + 2 * q + h;
+        float4 geo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int cr = 0; cr < 4; ++cr)
+          sre[h][cr] = sim[h][cr] = dre[h][cr] = dim[h][cr] = 0.0f;
+        if (b < half) {
+          float4 pa, pb, ma, mb, mgeo;
+          pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
+                      aterms, sg, pa, pb, geo);
+          pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
+                      spheroidal, aterms, sg, ma, mb, mgeo);
+          const float pr[4] = {pa.x, pa.z, pb.x, pb.z};
+          const float pi[4] = {pa.y, pa.w, pb.y, pb.w};
+          const float mr[4] = {ma.x, ma.z, mb.x, mb.z};
+          const float mi[4] = {ma.y, ma.w, mb.y, mb.w};
+#pragma unroll
+          for (int cr = 0; cr < 4; ++cr) {
+            sre[h][cr] = (pr[cr] + mr[cr]) * scale;
+            sim[h][cr] = (pi[cr] + mi[cr]) * scale;
+            dre[h][cr] = (pr[cr] - mr[cr]) * scale;
+            dim[h][cr] = (pi[cr] - mi[cr]) * scale;
+          }
+        }
+        geo_lds[2 * q + h] = geo;
+      }
+      // lane (g, col) of K-step ks: ks = q / 4, g = q % 4
+      uint2 *dst = bfr + (q >> 2) * 64 + (q & 3) * 16;
+#pragma unroll
+      for (int cl = 0; cl < 16; ++cl) {
+        const int cr = (cl & 7) >> 1;
+        const bool im = cl & 1;
+        const float bc0 = im ? sim[0][cr] : sre[0][cr];
+        const float bc1 = im ? sim[1][cr] : sre[1][cr];
+        const float bs0 = im ? dre[0][cr] : -dim[0][cr];
+        const float bs1 = im ? dre[1][cr] : -dim[1][cr];
+        dst[cl] = (cl & 8) ? make_uint2(split_lo(bc0, bc1), split_lo(bs0, bs1))
+                           : make_uint2(split_hi(bc0, bc1), split_hi(bs0, bs1));
+      }
+    }
+  };
+  if (single) {
+    build(0);
+    __syncthreads();
+  }
+
+  const floatx2 inv2pi = {kInv2PiHi, kInv2PiHi};
   for (int t0 = 0; t0 < nt; t0 += 64) {  // 4 waves x 16 timesteps
     const int t_row = t0 + wave * 16 + col;  // this lane's A row timestep
     const idg::UVWCoordinate<float> c = uvw[g.time_offset + min(t_row, nt - 1)];
     for (int cg0 = 0; cg0 < C; cg0 += CT) {
+      float kk[CT];
+#pragma unroll
+      for (int j = 0; j < CT; ++j) kk[j] = wavenumbers[min(cg0 + j, C - 1)];
       floatx4 acc[CT];
 #pragma unroll
       for (int j = 0; j < CT; ++j) acc[j] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 
-      for (int pc0 = 0; pc0 < half; pc0 += kPixChunk) {
-        const int cnt = min(kPixChunk, half - pc0);
-        __syncthreads();
-        for (int q = tid; q < kPixChunk; q += kBlock) {
-          const int ks = q >> 2, gq = q & 3;
-          if (q < cnt) {
-            const int b = pc0 + q;
-            float4 pa, pb, geo, ma, mb, mgeo;
-            pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
-                        aterms, sg, pa, pb, geo);
-            pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
-                        spheroidal, aterms, sg, ma, mb, mgeo);
-            geo_lds[q] = geo;
-            const float bv[8] = {pa.x, pa.y, pa.z, pa.w,
-                                 pb.x, pb.y, pb.z, pb.w};
-            const float mv[8] = {ma.x, ma.y, ma.z, ma.w,
-                                 mb.x, mb.y, mb.z, mb.w};
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc) {
-              const int pol = (cc & 7) >> 1;
-              uint2 d;
-              d.x = p_coeff(bv[2 * pol] * scale, bv[2 * pol + 1] * scale, cc,
-                            false);
-              d.y = p_coeff(mv[2 * pol] * scale, mv[2 * pol + 1] * scale, cc,
-                            true);
-              bfr[ks * 64 + gq * 16 + cc] = d;
-            }
-          } else {
-            geo_lds[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc)
-              bfr[ks * 64 + gq * 16 + cc] = make_uint2(0u, 0u);
-          }
+      for (int pc0 = 0; pc0 < half; pc0 += KP) {
+        if (!single) {
+          __syncthreads();
+          build(pc0);
+          __syncthreads();
         }
-        __syncthreads();
-        const int nks = (cnt + 3) / 4;
+        const int nks = (min(KP, half - pc0) + 7) / 8;
         for (int ks = 0; ks < nks; ++ks) {
-          const float4 geo = geo_lds[4 * ks + grp];
+          const float4 ga = geo_lds[8 * ks + 2 * grp];
+          const float4 gb = geo_lds[8 * ks + 2 * grp + 1];
           const uint2 bb = bfr[ks * 64 + lane];
           const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
           // phase_index = fma(u, l, v*m) + w*n with w = 0
-          const float pidx = fma_(c.u, geo.x, c.v * geo.y);
-          for (int jb = 0; jb < CT; jb += CB) {
-            const float ka = wavenumbers[min(cg0 + jb, C - 1)];
-            const float A = fma_(pidx, ka, -geo.w);
-            const float R = revolutions(A);
+          const floatx2 pidx = {fma_(c.u, ga.x, c.v * ga.y),
+                                fma_(c.u, gb.x, c.v * gb.y)};
+          const floatx2 npoff = {-ga.w, -gb.w};
 #pragma unroll
-            for (int j = jb; j < jb + CB && j < CT; ++j) {
-              const float k = wavenumbers[min(cg0 + j, C - 1)];
-              const float ph = fma_(pidx, k, -geo.w);
-              const float r = fma_(ph - A, kInv2PiHi, R);
-              float sn, cs;
-              sincos_rev(r, &sn, &cs);
-              unsigned hi, lo;
-              split_pair(cs, sn, &hi, &lo);
-              acc[j] = mfma16(pack4(hi, lo, hi, lo), bf, acc[j]);
+          for (int jb = 0; jb < CT; jb += CB) {
+            // anchor: phase at the block's first channel, in revolutions
+            const floatx2 A = __builtin_elementwise_fma(
+                pidx, floatx2{kk[jb], kk[jb]}, npoff);
+            const floatx2 ih = {kInv2PiHi, kInv2PiHi};
+            const floatx2 hi = A * ih;
+            floatx2 lo = __builtin_elementwise_fma(A, ih, -hi);
+            lo = __builtin_elementwise_fma(A, floatx2{kInv2PiLo, kInv2PiLo},
+                                           lo);
+            const floatx2 R =
+                (hi - floatx2{__builtin_rintf(hi.x), __builtin_rintf(hi.y)}) +
+                lo;
+#pragma unroll
+            for (int j = jb; j < jb + CB; ++j) {
+              const floatx2 ph = __builtin_elementwise_fma(
+                  pidx, floatx2{kk[j], kk[j]}, npoff);
+              const floatx2 r = __builtin_elementwise_fma(ph - A, inv2pi, R);
+              float s0, c0, s1, c1;
+              sincos_rev(r.x, &s0, &c0);
+              sincos_rev(r.y, &s1, &c1);
+              acc[j] = mfma16(split_quad(c0, c1, s0, s1), bf, acc[j]);
             }
           }
+          // one K-step's MFMAs stay in their iteration
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
 
@@ -248,10 +290,13 @@ __device__ __forceinline__ void degrid_mirror_mfma(
 
 }  // namespace
 
-// CG: channels per lane (VALU paths); IMPL: mirror path 0 = VALU, 1 = MFMA;
-// CT: channel tiles per MFMA pass.
-template <int S_CT, int CG, int IMPL, int CT>
-__global__ void __launch_bounds__(kBlock)
+// CG: channels per lane (VALU paths).
+// MODE: 0 = VALU kernel (every subgrid), 1 = MFMA kernel (mirror-eligible
+//       subgrids only, others untouched), 2 = fallback of the MFMA kernel
+//       (VALU paths, non-eligible subgrids only; 4 channels per lane).
+// CT: channels per MFMA pass.
+template <int S_CT, int CG, int MODE, int CT>
+__global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
     kernel_degridder_mi355x(const int grid_size, int subgrid_size,
                             float image_size, float w_step_in_lambda,
                             int nr_channels, int nr_stations,
@@ -262,17 +307,6 @@ __global__ void __launch_bounds__(kBlock)
                             const float2 *__restrict__ aterms,
                             const idg::Metadata *__restrict__ metadata,
                             const float2 *__restrict__ subgrids) {
-  // general: [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l,m,n,poff)
-  // mirror : [pair][0..1] = P'(base), [pair][2..3] = P'(mirror),
-  //          [pair][4] = geometry of the base pixel
-  // One LDS allocation shared by all paths (the MFMA path aliases it).
-  __shared__ float4 table[kChunk * 3];
-  static_assert(kPairChunk * 5 <= kChunk * 3, "table size");
-  static_assert(DegridMfmaLds::kWords <= kChunk * 3 * 4, "mfma lds size");
-  // The VALU paths of an MFMA build are fallbacks (w != 0, odd S): they use
-  // 4 channels per lane to keep the kernel's register budget low.
-  constexpr int CGV = IMPL == 1 ? 4 : CG;
-
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
   const int s = blockIdx.x;
@@ -281,23 +315,40 @@ __global__ void __launch_bounds__(kBlock)
                                        w_step_in_lambda);
   const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const int C = nr_channels;
-  const int ncg = (C + CGV - 1) / CGV;
-  const int nunits = g.nr_timesteps * ncg;
-  const bool mirror_ok = (S % 2 == 0) && g.w_offset == 0.0f;
 
-  if (IMPL == 1 && mirror_ok) {
-    // Subgrid-uniform: w = 0 on every timestep.
+  if constexpr (MODE != 0) {
+    // Subgrid-uniform mirror eligibility: even S, w_offset = 0 and w = 0 on
+    // every timestep (the MFMA kernel and its fallback split on it).
     bool w_nonzero = false;
     for (int t = tid; t < g.nr_timesteps; t += kBlock)
       w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-    if (__syncthreads_or(w_nonzero) == 0) {
-      degrid_mirror_mfma<S_CT, CT, 16>(g, S, npix, image_size, C, nr_stations,
-                                      uvw, wavenumbers, visibilities,
-                                      spheroidal, aterms, sg,
-                                      reinterpret_cast<unsigned *>(table));
+    const bool eligible = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
+                          g.w_offset == 0.0f;
+    if constexpr (MODE == 1) {
+      if (!eligible) return;
+      // whole subgrid (S = 32: 512 pairs) in one chunk, else 128-pair chunks
+      constexpr int KP = S_CT == 32 ? 512 : 128;
+      __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
+      degrid_mirror_mfma<S_CT, CT, 16, KP>(g, S, npix, image_size, C,
+                                          nr_stations, uvw, wavenumbers,
+                                          visibilities, spheroidal, aterms,
+                                          sg, lds);
       return;
     }
+    if (eligible) return;
   }
+
+  // general: [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l,m,n,poff)
+  // mirror : [pair][0..1] = P'(base), [pair][2..3] = P'(mirror),
+  //          [pair][4] = geometry of the base pixel
+  __shared__ float4 table[kChunk * 3];
+  static_assert(kPairChunk * 5 <= kChunk * 3, "table size");
+  // The fallback of an MFMA build only sees w != 0 / odd-S subgrids: it uses
+  // 4 channels per lane to keep its register budget low.
+  constexpr int CGV = MODE == 2 ? 4 : CG;
+  const int ncg = (C + CGV - 1) / CGV;
+  const int nunits = g.nr_timesteps * ncg;
+  const bool mirror_ok = (S % 2 == 0) && g.w_offset == 0.0f;
 
   for (int ubase = 0; ubase < nunits; ubase += kBlock) {
     const int unit = min(ubase + tid, nunits - 1);
@@ -401,8 +452,8 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-#define IDG_DEGRIDDER(S_, CG_, IMPL_) \
-  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_, IMPL_, 16>)
+#define IDG_DEGRIDDER(S_, CG_, MODE_) \
+  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_, MODE_, 16>)
 
 // IDG_DEGRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int degridder_impl() {
@@ -418,12 +469,16 @@ KernelChoice select_degridder(const Problem &p) {
   const bool cg8 = C % 8 == 0 || (C % 4 != 0 && C >= 8);
   const bool s32 = p.subgrid_size == 32, s64 = p.subgrid_size == 64;
   const bool mfma = degridder_impl() == 1;
-#define IDG_PICK(CG_)                                                      \
-  (mfma ? (s32 ? IDG_DEGRIDDER(32, CG_, 1)                                 \
-               : (s64 ? IDG_DEGRIDDER(64, CG_, 1) : IDG_DEGRIDDER(0, CG_, 1))) \
-        : (s32 ? IDG_DEGRIDDER(32, CG_, 0)                                 \
-               : (s64 ? IDG_DEGRIDDER(64, CG_, 0) : IDG_DEGRIDDER(0, CG_, 0))))
-  k.func = cg8 ? IDG_PICK(8) : IDG_PICK(4);
+#define IDG_PICK(CG_, MODE_)                                               \
+  (s32 ? IDG_DEGRIDDER(32, CG_, MODE_)                                     \
+       : (s64 ? IDG_DEGRIDDER(64, CG_, MODE_) : IDG_DEGRIDDER(0, CG_, MODE_)))
+  if (mfma) {
+    // the MFMA kernel has no CG; the fallback uses 4 channels per lane
+    k.func = IDG_PICK(4, 1);
+    k.fallback = IDG_PICK(4, 2);
+  } else {
+    k.func = cg8 ? IDG_PICK(8, 0) : IDG_PICK(4, 0);
+  }
 #undef IDG_PICK
   if (mfma)
     k.name = s32 ? "degridder_mi355x_s32"

@@ -386,13 +386,8 @@ __device__ __forceinline__ void grid_mirror_mfma(
                 sincos_rev(r01.y, &s1, &c1f);
                 sincos_rev(r23.x, &s2, &c2f);
                 sincos_rev(r23.y, &s3, &c3f);
-                unsigned hc01, lc01, hc23, lc23, hs01, ls01, hs23, ls23;
-                split_pair(c0f, c1f, &hc01, &lc01);
-                split_pair(c2f, c3f, &hc23, &lc23);
-                split_pair(s0, s1, &hs01, &ls01);
-                split_pair(s2, s3, &hs23, &ls23);
-                accx[i] = mfma16(pack4(hc01, lc01, hc23, lc23), bfx, accx[i]);
-                accy[i] = mfma16(pack4(hs01, ls01, hs23, ls23), bfy, accy[i]);
+                accx[i] = mfma16(split_quad(c0f, c1f, c2f, c3f), bfx, accx[i]);
+                accy[i] = mfma16(split_quad(s0, s1, s2, s3), bfy, accy[i]);
               }
               // Keep each K-step's MFMAs inside its own iteration.  When the
               // scheduler sank all of an iteration's MFMAs to the end of the
@@ -453,9 +448,11 @@ __device__ __forceinline__ void grid_mirror_mfma(
 
 // S_CT: subgrid size known at compile time (0 = runtime).
 // PPT : pixels per lane (VALU paths).   CB: channels per phase anchor.
-// IMPL: mirror-path implementation, 0 = VALU (v_pk_fma MAC), 1 = MFMA.
+// MODE: 0 = VALU kernel (VALU mirror path + general path, every subgrid),
+//       1 = MFMA kernel (mirror-eligible subgrids only, others untouched),
+//       2 = fallback of the MFMA kernel (general path, non-eligible only).
 // PT  : 16-pixel base tiles per wave in the MFMA path.
-template <int S_CT, int PPT, int CB, int IMPL, int PT>
+template <int S_CT, int PPT, int CB, int MODE, int PT>
 __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
                           float image_size, float w_step_in_lambda,
@@ -486,15 +483,17 @@ __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
   const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
                       g.w_offset == 0.0f;
 
-  if (IMPL == 1 && mirror) {
+  if constexpr (MODE == 1) {
+    if (!mirror) return;
     __shared__ unsigned lds[MfmaLds<PT>::kWords];
     grid_mirror_mfma<S_CT, PT, CB>(g, S, npix, image_size, C, nr_stations,
                                    uvw, wavenumbers, visibilities, spheroidal,
                                    aterms, out, lds);
     return;
   }
+  if (MODE == 2 && mirror) return;
 
-  if (mirror) {
+  if (MODE == 0 && mirror) {
     // Mirror-pair path: lane owns base pixels b (< npix/2) and npix-1-b.
     const int half = npix / 2;
     for (int tile = 0; tile < half; tile += kBlock * NB) {
@@ -559,9 +558,9 @@ __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
   }
 }
 
-#define IDG_GRIDDER(S_, PPT_, IMPL_)                                     \
+#define IDG_GRIDDER(S_, PPT_, MODE_)                                     \
   reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mi355x<S_, PPT_, 16, IMPL_, IDG_GRID_PT>)
+      &kernel_gridder_mi355x<S_, PPT_, 16, MODE_, IDG_GRID_PT>)
 
 // IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int gridder_impl() {
@@ -577,14 +576,17 @@ KernelChoice select_gridder(const Problem &p) {
   switch (p.subgrid_size) {
     case 32:
       k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
+      k.fallback = mfma ? IDG_GRIDDER(32, 4, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
       break;
     case 64:
       k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);
+      k.fallback = mfma ? IDG_GRIDDER(64, 4, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_s64" : "gridder_mi355x_s64_valu";
       break;
     default:
       k.func = mfma ? IDG_GRIDDER(0, 2, 1) : IDG_GRIDDER(0, 2, 0);
+      k.fallback = mfma ? IDG_GRIDDER(0, 2, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_generic" : "gridder_mi355x_generic_valu";
       break;
   }

@@ -40,15 +40,23 @@ __device__ __forceinline__ void split_pair(float c, float s, unsigned *hi,
   const f16x2 h = __builtin_convertvector(v, f16x2);
   const unsigned hu = __builtin_bit_cast(unsigned, h);
   unsigned lu;
-  asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]"
+  asm volatile("s_nop 0\n\tv_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]"
                : "=&v"(lu)
                : "v"(hu), "v"(c));
   asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] "
-               "op_sel_hi:[1,0,0]"
+               "op_sel_hi:[1,0,0]\n\ts_nop 1"
                : "+v"(lu)
                : "v"(hu), "v"(s));
   *hi = hu;
   *lo = lu;
+}
+
+// Four packed-f16 dwords as the 8-element MFMA operand.
+__device__ __forceinline__ half8 pack4(unsigned a, unsigned b, unsigned c,
+                                       unsigned d) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 v = {a, b, c, d};
+  return __builtin_bit_cast(half8, v);
 }
 
 // One f16 part of each of (a, b), packed: the hi part f16(x) where
@@ -70,17 +78,46 @@ __device__ __forceinline__ unsigned split_part(float a, float b, float m) {
   return r;
 }
 
+// hi parts (f16(a), f16(b)) packed.
+__device__ __forceinline__ unsigned split_hi(float a, float b) {
+  floatx2 v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
+}
+
+// lo parts (f16(a - f16(a)), f16(b - f16(b))) packed.
+__device__ __forceinline__ unsigned split_lo(float a, float b) {
+  unsigned hi, lo;
+  split_pair(a, b, &hi, &lo);
+  return lo;
+}
+
+// Two split_pair()s in one asm block: returns the MFMA operand dwords
+// (hi(a0, a1), lo(a0, a1), hi(b0, b1), lo(b0, b1)).  hipcc neither models
+// nor pads what is inside an asm string and adds only one wait state after
+// it, so the string carries its own pads: `s_nop 0` first (the inputs are
+// usually fresh v_sin/v_cos results: trans -> VALU forwarding needs 1 state)
+// and `s_nop 1` last (VALU write -> MFMA SrcA read needs 2 states; the
+// outputs are the next MFMA's A operand).
+__device__ __forceinline__ half8 split_quad(float a0, float a1, float b0,
+                                            float b1) {
+  unsigned h0, l0, h1, l1;
+  asm("s_nop 0\n\t"
+      "v_cvt_pk_f16_f32 %0, %4, %5\n\t"
+      "v_cvt_pk_f16_f32 %2, %6, %7\n\t"
+      "v_fma_mixlo_f16 %1, %0, -1.0, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, %2, -1.0, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %0, -1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, %2, -1.0, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(h0), "=&v"(l0), "=&v"(h1), "=&v"(l1)
+      : "v"(a0), "v"(a1), "v"(b0), "v"(b1));
+  return pack4(h0, l0, h1, l1);
+}
+
 __device__ __forceinline__ floatx4 mfma16(const half8 &a, const half8 &b,
                                           const floatx4 &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// Four packed-f16 dwords as the 8-element MFMA operand.
-__device__ __forceinline__ half8 pack4(unsigned a, unsigned b, unsigned c,
-                                       unsigned d) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 v = {a, b, c, d};
-  return __builtin_bit_cast(half8, v);
-}
 
 }  // namespace idg_mi355x
