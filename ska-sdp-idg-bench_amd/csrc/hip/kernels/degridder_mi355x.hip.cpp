@@ -37,7 +37,7 @@
 
 // waves-per-SIMD launch bound of the MFMA degridder (tuning knob)
 #ifndef IDG_DEGRID_WAVES
-#define IDG_DEGRID_WAVES 2
+#define IDG_DEGRID_WAVES 4
 #endif
 
 namespace idg_mi355x {
@@ -113,7 +113,7 @@ __device__ __forceinline__ void pixel_entry(
 // ---------------------------------------------------------------------------
 template <int KP>
 struct DegridMfmaLds {
-  static constexpr int kGeoWords = KP * 4;              // float4 per pair
+  static constexpr int kGeoWords = KP * 3;              // l | m | poff
   static constexpr int kBfrWords = (KP / 8) * 64 * 2;   // uint2 per lane
   static constexpr int kWords = kGeoWords + kBfrWords + 8;
 };
@@ -155,7 +155,10 @@ __device__ __forceinline__ void degrid_mirror_mfma(
   if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
   const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
 
-  float4 *geo_lds = reinterpret_cast<float4 *>(lds);
+  // pair geometry, structure of arrays: l[KP], m[KP], phase_offset[KP]
+  float *geo_l = reinterpret_cast<float *>(lds);
+  float *geo_m = geo_l + KP;
+  float *geo_o = geo_m + KP;
   uint2 *bfr = reinterpret_cast<uint2 *>(lds + L::kGeoWords);
   const bool single = half <= KP;
 
@@ -189,7 +192,9 @@ __device__ __forceinline__ void degrid_mirror_mfma(
             dim[h][cr] = (pi[cr] - mi[cr]) * scale;
           }
         }
-        geo_lds[2 * q + h] = geo;
+        geo_l[2 * q + h] = geo.x;
+        geo_m[2 * q + h] = geo.y;
+        geo_o[2 * q + h] = geo.w;
       }
       // lane (g, col) of K-step ks: ks = q / 4, g = q % 4
       uint2 *dst = bfr + (q >> 2) * 64 + (q & 3) * 16;
@@ -231,14 +236,16 @@ __device__ __forceinline__ void degrid_mirror_mfma(
         }
         const int nks = (min(KP, half - pc0) + 7) / 8;
         for (int ks = 0; ks < nks; ++ks) {
-          const float4 ga = geo_lds[8 * ks + 2 * grp];
-          const float4 gb = geo_lds[8 * ks + 2 * grp + 1];
+          const int pp = 8 * ks + 2 * grp;
+          const float2 gl = *reinterpret_cast<const float2 *>(geo_l + pp);
+          const float2 gm = *reinterpret_cast<const float2 *>(geo_m + pp);
+          const float2 go = *reinterpret_cast<const float2 *>(geo_o + pp);
           const uint2 bb = bfr[ks * 64 + lane];
           const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
           // phase_index = fma(u, l, v*m) + w*n with w = 0
-          const floatx2 pidx = {fma_(c.u, ga.x, c.v * ga.y),
-                                fma_(c.u, gb.x, c.v * gb.y)};
-          const floatx2 npoff = {-ga.w, -gb.w};
+          const floatx2 pidx = {fma_(c.u, gl.x, c.v * gm.x),
+                                fma_(c.u, gl.y, c.v * gm.y)};
+          const floatx2 npoff = {-go.x, -go.y};
 #pragma unroll
           for (int jb = 0; jb < CT; jb += CB) {
             // anchor: phase at the block's first channel, in revolutions
