@@ -359,12 +359,17 @@ __device__ __forceinline__ void grid_mirror_mfma(
               R2[i] = floatx2{r.x, r.x};
               R2[i + 1] = floatx2{r.y, r.y};
             }
-            for (int jj = jb; jj < je; ++jj) {
-              const int c0 = 4 * (j0 + jj);
-              const floatx2 k01 = {wavenumbers[min(c0, C - 1)],
-                                   wavenumbers[min(c0 + 1, C - 1)]};
-              const floatx2 k23 = {wavenumbers[min(c0 + 2, C - 1)],
-                                   wavenumbers[min(c0 + 3, C - 1)]};
+            // the block's CB wavenumbers, wave-uniform (SGPRs)
+            float kb[CB];
+#pragma unroll
+            for (int v = 0; v < CB; ++v)
+              kb[v] = wavenumbers[min(4 * (j0 + jb) + v, C - 1)];
+#pragma unroll
+            for (int u = 0; u < CB / 4; ++u) {
+              const int jj = jb + u;
+              if (jj >= je) break;
+              const floatx2 k01 = {kb[4 * u], kb[4 * u + 1]};
+              const floatx2 k23 = {kb[4 * u + 2], kb[4 * u + 3]};
               const int ks = qq * nj + jj;
               const uint4 bx = bbuf[(ks * 64 + lane) * 2];
               const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
