@@ -116,6 +116,16 @@ def traffic_for(path, workload, kernel):
         return None
 
 
+def issue_for(path, workload, kernel):
+    """VALU-issue utilisation of a kernel from its committed PMC summary."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t[workload][kernel].get("issue_bound")
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -213,12 +223,21 @@ def main():
         "traffic": traffic_for(args.traffic_file, args.workload,
                                kernels[dom]["kernel"]),
         "kernel": kernels[dom]["kernel"],
-        "note": ("FP32-compute-bound (VALU FMA + v_sin/v_cos; gfx950 FP32 "
-                 "vector peak = f32 MFMA peak = 157.3 TF); achieved = "
-                 "reference work model FLOPs per launch "
+        "note": ("achieved = reference work model FLOPs per launch "
                  f"({flops / nvis:.0f} FLOP/vis x {nvis} vis) / mean "
-                 "kernel duration (HIP events on the launch stream)"),
+                 "kernel duration (HIP events on the launch stream); peak = "
+                 "gfx950 FP32 peak (vector = f32 MFMA = 157.3 TF), the "
+                 "ceiling of the work model as the reference computes it. "
+                 "frac > 1 is possible: the complex MAC (32 of the model's "
+                 "~35 FLOP per pixel-visibility) runs on the f16 matrix "
+                 "core with a two-term f16 split at f32 accuracy, so the "
+                 "binding resource is VALU issue (exact phase, v_sin/v_cos, "
+                 "split), see issue_bound"),
     }
+    issue = issue_for(args.traffic_file, args.workload,
+                      kernels[dom]["kernel"])
+    if issue is not None:
+        roofline["issue_bound"] = issue
     roofline_hbm = {
         "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
         "achieved": round(nbytes / t_dom / 1e9, 2),
