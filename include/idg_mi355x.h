@@ -158,6 +158,40 @@ uint64_t idg_bytes_gridder(uint64_t nr_channels, uint64_t nr_timesteps,
                            uint64_t nr_subgrids, uint64_t subgrid_size,
                            uint64_t nr_correlations);
 
+/* ---- pipeline steps either side of the path ----
+ * Not in the reference (its Grid type is unused, app/common/types.hpp:358-370):
+ * these complete gridding into, and degridding from, a uv grid.  Conventions
+ * (DESIGN.md §8f):
+ *   gridding:   idg_gridder_launch -> idg_subgrid_fft_launch(+1, 1.0f)
+ *               -> idg_adder_launch
+ *   degridding: idg_splitter_launch -> idg_subgrid_fft_launch(-1, 1/S^2)
+ *               -> idg_degridder_launch
+ * grid: [nr_w_layers][4][grid_size][grid_size] complex64; a subgrid goes to
+ * layer metadata.coordinate.z.  Device pointers, asynchronous on `stream`.
+ */
+
+/* In-place 2-D DFT of each [S][S] correlation plane of subgrids
+ * [nr_subgrids][4][S][S]: out[k][l] = scale * sum in[y][x] *
+ * exp(sign * 2 pi i (k y + l x) / S); sign = +1 or -1. */
+int idg_subgrid_fft_launch(int nr_subgrids, int subgrid_size, int sign,
+                           float scale, idg_cfloat_t *subgrids, void *stream);
+
+/* grid[z][pol][y0 + y][x0 + x] += exp(i pi ((x + y)(S + 1)/S - 1)) *
+ * subgrid[s][pol][(y + S/2) % S][(x + S/2) % S]; subgrids not wholly inside
+ * the grid are skipped.  Float atomics: summation order not deterministic. */
+int idg_adder_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                     int nr_w_layers, const idg_metadata_t *metadata,
+                     const idg_cfloat_t *subgrids, idg_cfloat_t *grid,
+                     void *stream);
+
+/* The adjoint placement: subgrid[s][pol][(y + S/2) % S][(x + S/2) % S] =
+ * exp(-i pi ((x + y)(S + 1)/S - 1)) * grid[z][pol][y0 + y][x0 + x]; zero for
+ * subgrids not wholly inside the grid. */
+int idg_splitter_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                        int nr_w_layers, const idg_metadata_t *metadata,
+                        const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
+                        void *stream);
+
 /* ---- synthetic observation (app/common/init.cpp:4-180) -------------------
  * Exactly the reference harness' inputs: srand(0), then the initialize_*
  * generators in harness order.  nr_subgrids = nr_stations*(nr_stations-1)/2

@@ -99,6 +99,48 @@ int idg_abi_version(void) { return IDG_MI355X_ABI_VERSION; }
 
 const char *idg_last_error(void) { return g_last_error.c_str(); }
 
+int idg_subgrid_fft_launch(int nr_subgrids, int subgrid_size, int sign,
+                           float scale, idg_cfloat_t *subgrids, void *stream) {
+  if (nr_subgrids < 0 || subgrid_size <= 0 || subgrid_size > 64 ||
+      (sign != 1 && sign != -1))
+    return fail(IDG_E_INVALID_ARGUMENT,
+                "nr_subgrids >= 0, 0 < subgrid_size <= 64, sign = +1 or -1");
+  return from_hip(idg_mi355x::launch_subgrid_fft(
+                      nr_subgrids, subgrid_size, sign, scale, subgrids,
+                      static_cast<hipStream_t>(stream)),
+                  "idg_subgrid_fft_launch");
+}
+
+int idg_adder_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                     int nr_w_layers, const idg_metadata_t *metadata,
+                     const idg_cfloat_t *subgrids, idg_cfloat_t *grid,
+                     void *stream) {
+  if (nr_subgrids < 0 || subgrid_size <= 0 || subgrid_size % 2 ||
+      grid_size < subgrid_size || nr_w_layers <= 0)
+    return fail(IDG_E_INVALID_ARGUMENT,
+                "even subgrid_size <= grid_size, nr_w_layers > 0 required");
+  return from_hip(idg_mi355x::launch_adder(
+                      nr_subgrids, grid_size, subgrid_size, nr_w_layers,
+                      metadata, subgrids, grid,
+                      static_cast<hipStream_t>(stream)),
+                  "idg_adder_launch");
+}
+
+int idg_splitter_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                        int nr_w_layers, const idg_metadata_t *metadata,
+                        const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
+                        void *stream) {
+  if (nr_subgrids < 0 || subgrid_size <= 0 || subgrid_size % 2 ||
+      grid_size < subgrid_size || nr_w_layers <= 0)
+    return fail(IDG_E_INVALID_ARGUMENT,
+                "even subgrid_size <= grid_size, nr_w_layers > 0 required");
+  return from_hip(idg_mi355x::launch_splitter(
+                      nr_subgrids, grid_size, subgrid_size, nr_w_layers,
+                      metadata, grid, subgrids,
+                      static_cast<hipStream_t>(stream)),
+                  "idg_splitter_launch");
+}
+
 int idg_c_run_gridder(int nr_subgrids, int grid_size, int subgrid_size,
                       float image_size, float w_step_in_lambda,
                       int nr_channels, int nr_stations, const idg_uvw_t *uvw,

@@ -1,0 +1,208 @@
+// pipeline_mi355x.hip.cpp -- the IDG steps either side of the gridder and
+// degridder: batched subgrid FFT, adder
+// (subgrids -> uv grid) and splitter (uv grid -> subgrids).
+//
+// None of these is in the reference (its `Grid` type, types.hpp:358-370, is
+// never used), so their conventions are pinned by the path they complete
+// (tests/test_pipeline*.py):
+//
+//   gridding:   gridder -> FFT(sign +1, scale 1) -> adder
+//   degridding: splitter -> FFT(sign -1, scale 1/S^2) -> degridder
+//
+// with, for subgrid pixel (y, x) at grid cell (coordinate.y + y,
+// coordinate.x + x) and FFT index ((y + S/2) % S, (x + S/2) % S),
+//   adder:    grid  += exp(+i pi ((x + y)(S + 1)/S - 1)) * F
+//   splitter: F      = exp(-i pi ((x + y)(S + 1)/S - 1)) * grid
+// so that one unit visibility whose uv lies exactly on a grid cell grids to
+// S^2 at that cell, and a unit grid cell degrids to 1 for a visibility at it
+// (checked against the C oracle's gridder/degridder).
+//
+// The grid is [nr_w_layers][4][G][G] complex64; a subgrid goes to layer
+// coordinate.z (w-stacking).  A subgrid that does not lie wholly inside the
+// grid is skipped by the adder and zero-filled by the splitter.
+#include <hip/hip_runtime.h>
+
+#include "../util.hpp"
+#include "common/types.hpp"
+#include "device.hpp"
+
+namespace idg_mi355x {
+
+namespace {
+
+// exp(sign * 2 pi i * n / d) for integers, argument reduced exactly.
+__device__ __forceinline__ float2 unit_phasor(int n, int d, float sign) {
+  int r = n % d;
+  if (r < 0) r += d;
+  const float rev = static_cast<float>(r) / static_cast<float>(d);
+  return make_float2(__builtin_amdgcn_cosf(rev),
+                     sign * __builtin_amdgcn_sinf(rev));
+}
+
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+  return make_float2(fma_(a.x, b.x, -(a.y * b.y)), fma_(a.x, b.y, a.y * b.x));
+}
+
+// Adder/splitter phasor of subgrid pixel (y, x): exp(i sgn pi ((x + y)(S + 1)
+// / S - 1)) = exp(2 pi i sgn ((x + y)(S + 1) - S) / (2 S)).
+__device__ __forceinline__ float2 shift_phasor(int x, int y, int S, float sgn) {
+  return unit_phasor((x + y) * (S + 1) - S, 2 * S, sgn);
+}
+
+__device__ __forceinline__ bool fits(const idg::Metadata &m, int G, int S,
+                                     int nr_w_layers) {
+  return m.coordinate.x >= 0 && m.coordinate.x + S <= G &&
+         m.coordinate.y >= 0 && m.coordinate.y + S <= G &&
+         m.coordinate.z >= 0 && m.coordinate.z < nr_w_layers;
+}
+
+}  // namespace
+
+// 2-D DFT of one S x S correlation plane per workgroup, in place:
+//   out[k][l] = scale * sum_{y,x} in[y][x] exp(sign 2 pi i (k y + l x) / S)
+// as a row pass then a column pass through LDS, twiddles from a per-plane
+// table (exact integer argument reduction).  Unnormalised for scale = 1
+// (numpy: sign -1 -> fft2, sign +1 -> ifft2 * S^2).  Dynamic LDS:
+// (2 S^2 + S) float2.
+__global__ void __launch_bounds__(256)
+    kernel_subgrid_dft(float2 *__restrict__ planes, int S, float sign,
+                       float scale) {
+  extern __shared__ float2 dft_lds[];
+  float2 *a = dft_lds;
+  float2 *b = a + S * S;
+  float2 *tw = b + S * S;
+  float2 *plane = planes + static_cast<size_t>(blockIdx.x) * S * S;
+  const int tid = threadIdx.x;
+  const int npix = S * S;
+  for (int i = tid; i < S; i += blockDim.x) tw[i] = unit_phasor(i, S, sign);
+  for (int i = tid; i < npix; i += blockDim.x) a[i] = plane[i];
+  __syncthreads();
+  // rows: b[y][l] = sum_x a[y][x] tw[(x l) mod S]
+  for (int i = tid; i < npix; i += blockDim.x) {
+    const int y = i / S, l = i - y * S;
+    float re = 0.0f, im = 0.0f;
+    int idx = 0;
+    for (int x = 0; x < S; ++x) {
+      const float2 v = a[y * S + x], w = tw[idx];
+      re = fma_(v.x, w.x, fma_(-v.y, w.y, re));
+      im = fma_(v.x, w.y, fma_(v.y, w.x, im));
+      idx += l;
+      if (idx >= S) idx -= S;
+    }
+    b[i] = make_float2(re, im);
+  }
+  __syncthreads();
+  // columns: out[k][l] = scale * sum_y b[y][l] tw[(y k) mod S]
+  for (int i = tid; i < npix; i += blockDim.x) {
+    const int k = i / S, l = i - k * S;
+    float re = 0.0f, im = 0.0f;
+    int idx = 0;
+    for (int y = 0; y < S; ++y) {
+      const float2 v = b[y * S + l], w = tw[idx];
+      re = fma_(v.x, w.x, fma_(-v.y, w.y, re));
+      im = fma_(v.x, w.y, fma_(v.y, w.x, im));
+      idx += k;
+      if (idx >= S) idx -= S;
+    }
+    plane[i] = make_float2(re * scale, im * scale);
+  }
+}
+
+// grid[z][pol][cy + y][cx + x] += shift_phasor(x, y) * F[s][pol][ys][xs],
+// ys = (y + S/2) % S, xs = (x + S/2) % S.  Overlapping subgrids meet in
+// float atomics (order, hence the last bits, not deterministic).
+__global__ void __launch_bounds__(256)
+    kernel_adder(const idg::Metadata *__restrict__ metadata,
+                 const float2 *__restrict__ subgrids,
+                 float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
+  const int s = blockIdx.x;
+  const idg::Metadata m = metadata[s];
+  if (!fits(m, G, S, nr_w_layers)) return;
+  const int npix = S * S;
+  const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
+  float *g = reinterpret_cast<float *>(
+      grid + static_cast<size_t>(m.coordinate.z) * 4 * G * G);
+  for (int i = threadIdx.x; i < npix; i += blockDim.x) {
+    const int y = i / S, x = i - y * S;
+    const int src = ((y + S / 2) % S) * S + (x + S / 2) % S;
+    const float2 ph = shift_phasor(x, y, S, 1.0f);
+    const size_t dst =
+        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+#pragma unroll
+    for (int pol = 0; pol < 4; ++pol) {
+      const float2 v = cmulf(ph, sg[pol * npix + src]);
+      const size_t o = 2 * (static_cast<size_t>(pol) * G * G + dst);
+      unsafeAtomicAdd(g + o, v.x);
+      unsafeAtomicAdd(g + o + 1, v.y);
+    }
+  }
+}
+
+// F[s][pol][ys][xs] = conj(shift_phasor(x, y)) * grid[z][pol][cy + y][cx + x]
+// (zero when the subgrid does not lie inside the grid).
+__global__ void __launch_bounds__(256)
+    kernel_splitter(const idg::Metadata *__restrict__ metadata,
+                    const float2 *__restrict__ grid,
+                    float2 *__restrict__ subgrids, int G, int S,
+                    int nr_w_layers) {
+  const int s = blockIdx.x;
+  const idg::Metadata m = metadata[s];
+  const bool inside = fits(m, G, S, nr_w_layers);
+  const int npix = S * S;
+  float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
+  const float2 *gz =
+      grid + static_cast<size_t>(inside ? m.coordinate.z : 0) * 4 * G * G;
+  for (int i = threadIdx.x; i < npix; i += blockDim.x) {
+    const int y = i / S, x = i - y * S;
+    const int dst = ((y + S / 2) % S) * S + (x + S / 2) % S;
+    const float2 ph = shift_phasor(x, y, S, -1.0f);
+    const size_t src =
+        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+#pragma unroll
+    for (int pol = 0; pol < 4; ++pol)
+      sg[pol * npix + dst] =
+          inside ? cmulf(ph, gz[static_cast<size_t>(pol) * G * G + src])
+                 : make_float2(0.0f, 0.0f);
+  }
+}
+
+hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
+                              float scale, void *d_subgrids,
+                              hipStream_t stream) {
+  if (nr_subgrids <= 0) return hipSuccess;
+  const int S = subgrid_size;
+  const size_t lds = (2 * static_cast<size_t>(S) * S + S) * sizeof(float2);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kernel_subgrid_dft, dim3(4 * nr_subgrids), dim3(256),
+                     lds, stream, static_cast<float2 *>(d_subgrids), S,
+                     sign >= 0 ? 1.0f : -1.0f, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
+                        int nr_w_layers, const void *d_metadata,
+                        const void *d_subgrids, void *d_grid,
+                        hipStream_t stream) {
+  if (nr_subgrids <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kernel_adder, dim3(nr_subgrids), dim3(256), 0, stream,
+                     static_cast<const idg::Metadata *>(d_metadata),
+                     static_cast<const float2 *>(d_subgrids),
+                     static_cast<float2 *>(d_grid), grid_size, subgrid_size,
+                     nr_w_layers);
+  return hipGetLastError();
+}
+
+hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
+                           int nr_w_layers, const void *d_metadata,
+                           const void *d_grid, void *d_subgrids,
+                           hipStream_t stream) {
+  if (nr_subgrids <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0, stream,
+                     static_cast<const idg::Metadata *>(d_metadata),
+                     static_cast<const float2 *>(d_grid),
+                     static_cast<float2 *>(d_subgrids), grid_size,
+                     subgrid_size, nr_w_layers);
+  return hipGetLastError();
+}
+
+}  // namespace idg_mi355x

@@ -144,6 +144,19 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
                     void *subgrids, std::string *msg,
                     const KernelChoice *force = nullptr);
 
+// Pipeline steps (kernels/pipeline_mi355x.hip.cpp; include/idg_mi355x.h).
+hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
+                              float scale, void *d_subgrids,
+                              hipStream_t stream);
+hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
+                        int nr_w_layers, const void *d_metadata,
+                        const void *d_subgrids, void *d_grid,
+                        hipStream_t stream);
+hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
+                           int nr_w_layers, const void *d_metadata,
+                           const void *d_grid, void *d_subgrids,
+                           hipStream_t stream);
+
 // Perf entry shared by p_run_gridder_/p_run_degridder_: env-configured
 // problem, synthetic inputs, timed launches.  Returns seconds per launch.
 double run_performance(Direction dir, const void *func, std::string name,

@@ -44,6 +44,9 @@ SIGNATURES = {
     "idg_bytes_gridder": (_U64, [_U64, _U64, _U64, _U64, _U64]),
     "idg_generate": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P,
                           _P, _I]),
+    "idg_subgrid_fft_launch": (_I, [_I, _I, _I, _F, _P, _P]),
+    "idg_adder_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "idg_splitter_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
 }
 
 

@@ -234,6 +234,87 @@ def degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
 
 
 # ---------------------------------------------------------------------------
+# Pipeline steps either side of the path (not in the
+# reference).  gridding:   gridder -> subgrid_fft(+1) -> adder
+#              degridding: splitter -> subgrid_fft(-1, 1/S^2) -> degridder
+# ---------------------------------------------------------------------------
+def subgrid_fft_launch(subgrids, sign, scale=1.0, stream=None):
+    """In-place 2-D DFT of every [S][S] correlation plane of a float32
+    [NS, 4, S, S, 2] tensor: out = scale * sum in * exp(sign 2 pi i ...)."""
+    import torch
+    ns, _, S = subgrids.shape[0], subgrids.shape[1], subgrids.shape[2]
+    _check(lib.idg_subgrid_fft_launch(
+        ns, S, int(sign), float(scale),
+        _dev_ptr(subgrids, "subgrids", torch.float32), _stream_handle(stream)),
+        "subgrid_fft_launch")
+
+
+def adder_launch(grid_size, metadata, subgrids, grid, nr_w_layers=1,
+                 stream=None):
+    """grid [W, 4, G, G, 2] float32 += the FFT'd subgrids placed at their
+    metadata coordinates (float atomics)."""
+    import torch
+    ns, S = subgrids.shape[0], subgrids.shape[2]
+    _check(lib.idg_adder_launch(
+        ns, grid_size, S, nr_w_layers, _dev_ptr(metadata, "metadata"),
+        _dev_ptr(subgrids, "subgrids", torch.float32),
+        _dev_ptr(grid, "grid", torch.float32), _stream_handle(stream)),
+        "adder_launch")
+
+
+def splitter_launch(grid_size, metadata, grid, subgrids, nr_w_layers=1,
+                    stream=None):
+    """subgrids [NS, 4, S, S, 2] = the uv cells under each subgrid (adjoint
+    of adder_launch's placement)."""
+    import torch
+    ns, S = subgrids.shape[0], subgrids.shape[2]
+    _check(lib.idg_splitter_launch(
+        ns, grid_size, S, nr_w_layers, _dev_ptr(metadata, "metadata"),
+        _dev_ptr(grid, "grid", torch.float32),
+        _dev_ptr(subgrids, "subgrids", torch.float32), _stream_handle(stream)),
+        "splitter_launch")
+
+
+def grid_onto(nr_subgrids, grid_size, subgrid_size, image_size,
+              w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
+              visibilities, spheroidal, aterms, metadata, grid,
+              nr_w_layers=1, subgrids=None, stream=None):
+    """Visibilities -> uv grid: gridder, subgrid FFT (+1), adder into
+    `grid` (accumulates).  Returns the (uv-domain) subgrid scratch."""
+    import torch
+    if subgrids is None:
+        subgrids = torch.empty((nr_subgrids, 4, subgrid_size, subgrid_size, 2),
+                               dtype=torch.float32, device=grid.device)
+    gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                   w_step_in_lambda, nr_channels, nr_stations, uvw,
+                   wavenumbers, visibilities, spheroidal, aterms, metadata,
+                   subgrids, stream)
+    subgrid_fft_launch(subgrids, +1, 1.0, stream)
+    adder_launch(grid_size, metadata, subgrids, grid, nr_w_layers, stream)
+    return subgrids
+
+
+def degrid_from(nr_subgrids, grid_size, subgrid_size, image_size,
+                w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
+                visibilities, spheroidal, aterms, metadata, grid,
+                nr_w_layers=1, subgrids=None, stream=None):
+    """uv grid -> visibilities: splitter, subgrid FFT (-1, 1/S^2), degridder
+    (overwrites the visibility rows of every subgrid)."""
+    import torch
+    if subgrids is None:
+        subgrids = torch.empty((nr_subgrids, 4, subgrid_size, subgrid_size, 2),
+                               dtype=torch.float32, device=grid.device)
+    splitter_launch(grid_size, metadata, grid, subgrids, nr_w_layers, stream)
+    subgrid_fft_launch(subgrids, -1, 1.0 / (subgrid_size * subgrid_size),
+                       stream)
+    degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                     w_step_in_lambda, nr_channels, nr_stations, uvw,
+                     wavenumbers, visibilities, spheroidal, aterms, metadata,
+                     subgrids, stream)
+    return subgrids
+
+
+# ---------------------------------------------------------------------------
 # Perf entries, device info, work model
 # ---------------------------------------------------------------------------
 def p_run_gridder():

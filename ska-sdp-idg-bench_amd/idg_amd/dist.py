@@ -1,8 +1,10 @@
 """One process per GPU: rank setup and the few collectives the driver needs.
 
 The gridder/degridder data path has no collective (subgrids shard with no
-exchange, idg_amd.shard); torch.distributed is used only for the bench's
-barrier / max-over-ranks timing and for optional gathers of shard outputs.
+exchange, idg_amd.shard); torch.distributed is used for the bench's
+barrier / max-over-ranks timing, optional gathers of shard outputs, and the
+one real exchange step of the pipeline: summing the ranks' partial uv grids
+(reduce_grid, SURVEY.md §8e "final grid-sum").
 Backend "nccl" is RCCL on ROCm (over xGMI); "gloo" runs the same code on CPU.
 """
 import os
@@ -87,3 +89,17 @@ def gather_shards(local, counts):
 def finalize():
     if torch_dist.is_initialized():
         torch_dist.destroy_process_group()
+
+
+def reduce_grid(grid, to_all=True):
+    """Sum the ranks' partial uv grids in place (one RCCL all-reduce, or a
+    reduce to rank 0 when to_all is False).  The grid is one contiguous
+    [W, 4, G, G, 2] float32 tensor (32 MiB per w-layer at G = 1024), so this
+    is a single large collective, ring-bound by the xGMI links."""
+    if not torch_dist.is_initialized():
+        return grid
+    if to_all:
+        torch_dist.all_reduce(grid, op=torch_dist.ReduceOp.SUM)
+    else:
+        torch_dist.reduce(grid, dst=0, op=torch_dist.ReduceOp.SUM)
+    return grid

@@ -80,3 +80,61 @@ def test_gloo_world2_sharded_gridder_equals_single_process(tmp_path,
     assert np.array_equal(got, ref)
     tmax, tsum = open(path + ".txt").read().split()
     assert float(tmax) == 2.0 and float(tsum) == 2.0
+
+
+def _grid_worker(rank, world, port, result_path):
+    """Each rank grids its shard (oracle gridder + numpy FFT/adder standing
+    in for the GPU steps) onto a partial uv grid; reduce_grid sums them."""
+    import sys
+    for p in (PKG, ORACLE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import idg_amd
+    from idg_amd import dist, shard
+    import oracle as orc
+    import pipeline_oracle as pl
+    r, _, w = dist.init(backend="gloo")
+    st, ts, T, C, G, S = 4, 3, 6, 3, 256, 16
+    a = idg_amd.generate(st, ts, T, C, G, S)
+    md = a["metadata"]
+    s0, s1 = shard.plan_shards(md, w)[r]
+    sub, r0, r1 = shard.shard(md, s0, s1)
+    out = np.zeros((s1 - s0, 4, S, S, 2), np.float32)
+    uvw = np.ascontiguousarray(a["uvw"].reshape(-1, 3)[r0:r1])
+    vis = np.ascontiguousarray(a["visibilities"].reshape(-1, C, 4, 2)[r0:r1])
+    orc.Oracle().gridder(s1 - s0, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st, uvw,
+                         a["wavenumbers"], vis, a["spheroidal"], a["aterms"],
+                         sub, out)
+    part = pl.adder(np.zeros((1, 4, G, G), complex), sub,
+                    pl.subgrid_fft(pl.to_complex(out), +1))
+    grid = torch.from_numpy(np.ascontiguousarray(pl.to_pairs(part)))
+    dist.reduce_grid(grid)
+    if r == 0:
+        np.save(result_path, grid.numpy())
+    dist.finalize()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_grid_reduce_equals_single_process(tmp_path, oracle_lib):
+    """The pipeline's one exchange step (SURVEY.md §8e final grid-sum): the
+    sum of the ranks' partial grids equals gridding every subgrid at once."""
+    import idg_amd
+    import pipeline_oracle as pl
+    port = _free_port()
+    path = str(tmp_path / "grid.npy")
+    mp.start_processes(_grid_worker, args=(2, port, path), nprocs=2,
+                       join=True, start_method="spawn")
+    got = pl.to_complex(np.load(path))
+    st, ts, T, C, G, S = 4, 3, 6, 3, 256, 16
+    a = idg_amd.generate(st, ts, T, C, G, S)
+    ns = a["metadata"].size
+    sg = np.zeros((ns, 4, S, S, 2), np.float32)
+    oracle_lib.gridder(ns, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st, a["uvw"],
+                       a["wavenumbers"], a["visibilities"], a["spheroidal"],
+                       a["aterms"], a["metadata"], sg)
+    ref = pl.adder(np.zeros((1, 4, G, G), complex), a["metadata"],
+                   pl.subgrid_fft(pl.to_complex(sg), +1))
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
