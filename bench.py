@@ -60,6 +60,8 @@ def parse():
                     help="override NR_TIMESLOTS (batch size)")
     ap.add_argument("--cpu-sample-subgrids", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip timing the FFT / adder / grid-sum / splitter")
     ap.add_argument("--traffic-file", default=os.path.join(
         REPO, "profiles", "traffic.json"))
     return ap.parse_args()
@@ -247,6 +249,66 @@ def main():
                  "FLOP/B, so <= ~5.5% by construction"),
     }
 
+    # ---- pipeline steps around the path (not in `value`): subgrid FFT,
+    # adder onto the uv grid, the multi-GPU grid-sum over RCCL (the one
+    # exchange step, BASELINE configs[3]), splitter, inverse FFT ----------
+    pipeline = None
+    if not args.no_pipeline:
+        gridt = torch.zeros((1, 4, G, G, 2), dtype=torch.float32,
+                            device="cuda")
+        uvsub = torch.empty_like(grid_out)
+        npipe = max(1, min(args.steps, 5))
+        pev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)]
+               for _ in range(npipe)]
+        for it in range(npipe + 1):
+            e = pev[it - 1] if it > 0 else None
+            uvsub.copy_(grid_out)
+            gridt.zero_()
+            dist.barrier()
+            if e:
+                e[0].record(stream)
+            idg_amd.subgrid_fft_launch(uvsub, +1, 1.0, stream=stream)
+            if e:
+                e[1].record(stream)
+            idg_amd.adder_launch(G, dev["metadata"], uvsub, gridt,
+                                 stream=stream)
+            if e:
+                e[2].record(stream)
+            dist.reduce_grid(gridt)
+            if e:
+                e[3].record(stream)
+            idg_amd.splitter_launch(G, dev["metadata"], gridt, uvsub,
+                                    stream=stream)
+            if e:
+                e[4].record(stream)
+            idg_amd.subgrid_fft_launch(uvsub, -1, 1.0 / (S * S),
+                                       stream=stream)
+            if e:
+                e[5].record(stream)
+        torch.cuda.synchronize()
+
+        def avg(i, j):
+            return dist.max_over_ranks(
+                sum(e[i].elapsed_time(e[j]) for e in pev) / npipe)
+        pipeline = {
+            "fft_ms": round(avg(0, 1), 4),
+            "adder_ms": round(avg(1, 2), 4),
+            "grid_reduce_ms": round(avg(2, 3), 4),
+            "splitter_ms": round(avg(3, 4), 4),
+            "ifft_ms": round(avg(4, 5), 4),
+            "grid": f"[1][4][{G}][{G}] complex64, {G * G * 32 / 2**20:.0f} MiB",
+            "grid_reduce": ("all_reduce(sum) over RCCL/xGMI" if world > 1
+                            else "single rank: no collective"),
+        }
+        extra = sum(pipeline[k] for k in ("fft_ms", "adder_ms",
+                                          "grid_reduce_ms", "splitter_ms",
+                                          "ifft_ms")) / 1e3
+        pipeline["full_cycle_mvis_s"] = round(
+            world * nvis / (sec_per_step + extra) / 1e6, 2)
+        pipeline["note"] = ("gridder -> FFT -> adder -> grid-sum and "
+                            "splitter -> FFT -> degridder around the timed "
+                            "step; reported beside `value`, not in it")
+
     result = {
         "metric": METRIC,
         "value": round(world * nvis / sec_per_step / 1e6, 2),
@@ -277,6 +339,7 @@ def main():
         "kernels": kernels,
         "roofline": roofline,
         "roofline_hbm": roofline_hbm,
+        "pipeline": pipeline,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
