@@ -166,16 +166,83 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Power-of-two S: radix-2 Stockham FFT (log2 S stages per direction, natural
+// order in and out) through two LDS buffers, the same transform as
+// kernel_subgrid_dft.  Twiddles w^k = exp(sign 2 pi i k / S), k < S/2, from
+// an LDS table.  Dynamic LDS: (2 S^2 + S/2) float2.
+__global__ void __launch_bounds__(256)
+    kernel_subgrid_fft2(float2 *__restrict__ planes, int S, int log2S,
+                        float sign, float scale) {
+  extern __shared__ float2 fft_lds[];
+  float2 *buf0 = fft_lds;
+  float2 *buf1 = buf0 + S * S;
+  float2 *tw = buf1 + S * S;
+  float2 *plane = planes + static_cast<size_t>(blockIdx.x) * S * S;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int npix = S * S, half = S / 2;
+  for (int i = tid; i < half; i += nthr) tw[i] = unit_phasor(i, S, sign);
+  for (int i = tid; i < npix; i += nthr) buf0[i] = plane[i];
+  __syncthreads();
+  float2 *src = buf0, *dst = buf1;
+  // pass 0: rows (element stride 1, sequence stride S); pass 1: columns
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const int es = pass == 0 ? 1 : S, ss = pass == 0 ? S : 1;
+#pragma unroll 1
+    for (int st = 0; st < log2S; ++st) {
+      const int ns = 1 << st;           // current sub-transform length
+      const int tstep = half >> st;     // twiddle index step S/(2 ns)
+      for (int b = tid; b < npix / 2; b += nthr) {
+        // consecutive lanes take consecutive elements (rows) or consecutive
+        // sequences (columns): unit LDS stride, no bank conflicts
+        int seq, j;
+        if (pass == 0) {
+          seq = b / half;
+          j = b - seq * half;
+        } else {
+          j = b / S;
+          seq = b - j * S;
+        }
+        const int k = j & (ns - 1);
+        const int base = seq * ss;
+        const float2 a0 = src[base + j * es];
+        const float2 a1 = cmulf(src[base + (j + half) * es], tw[k * tstep]);
+        const int d = ((j - k) << 1) + k;
+        dst[base + d * es] = make_float2(a0.x + a1.x, a0.y + a1.y);
+        dst[base + (d + ns) * es] = make_float2(a0.x - a1.x, a0.y - a1.y);
+      }
+      __syncthreads();
+      float2 *t = src;
+      src = dst;
+      dst = t;
+    }
+  }
+  for (int i = tid; i < npix; i += nthr)
+    plane[i] = make_float2(src[i].x * scale, src[i].y * scale);
+}
+
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
                               float scale, void *d_subgrids,
                               hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
   const int S = subgrid_size;
+  const float sgn = sign >= 0 ? 1.0f : -1.0f;
+  if ((S & (S - 1)) == 0 && S >= 2) {
+    int log2S = 0;
+    while ((1 << log2S) < S) ++log2S;
+    const size_t lds = (2 * static_cast<size_t>(S) * S + S / 2) *
+                       sizeof(float2);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kernel_subgrid_fft2, dim3(4 * nr_subgrids), dim3(256),
+                       lds, stream, static_cast<float2 *>(d_subgrids), S,
+                       log2S, sgn, scale);
+    return hipGetLastError();
+  }
   const size_t lds = (2 * static_cast<size_t>(S) * S + S) * sizeof(float2);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kernel_subgrid_dft, dim3(4 * nr_subgrids), dim3(256),
-                     lds, stream, static_cast<float2 *>(d_subgrids), S,
-                     sign >= 0 ? 1.0f : -1.0f, scale);
+                     lds, stream, static_cast<float2 *>(d_subgrids), S, sgn,
+                     scale);
   return hipGetLastError();
 }
 
