@@ -184,12 +184,16 @@ def main():
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
               for _ in range(args.steps)]
+    from idg_amd.energy import EnergyMeter
+    meter = EnergyMeter(local_rank)
     dist.barrier()
     torch.cuda.synchronize()
+    meter.start()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
     torch.cuda.synchronize()
+    joules = meter.stop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = dist.max_over_ranks(elapsed)
@@ -309,6 +313,19 @@ def main():
                             "splitter -> FFT -> degridder around the timed "
                             "step; reported beside `value`, not in it")
 
+    # ---- energy over the timed region (amdsmi accumulated-energy counter;
+    # the reference's PowerSensor report, app/HIP/util.cpp:134-159) --------
+    energy = None
+    if joules is not None and joules > 0:
+        j_all = dist.sum_over_ranks(joules)
+        energy = {
+            "joules_per_step": round(j_all / args.steps, 4),
+            "avg_power_w_per_gpu": round(j_all / world / elapsed, 1),
+            "mvis_per_joule": round(world * nvis * args.steps / j_all / 1e6,
+                                    3),
+            "source": "amdsmi_get_energy_count over the timed steps",
+        }
+
     result = {
         "metric": METRIC,
         "value": round(world * nvis / sec_per_step / 1e6, 2),
@@ -340,6 +357,7 @@ def main():
         "roofline": roofline,
         "roofline_hbm": roofline_hbm,
         "pipeline": pipeline,
+        "energy": energy,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
