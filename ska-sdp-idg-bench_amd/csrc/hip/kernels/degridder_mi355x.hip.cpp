@@ -125,7 +125,8 @@ __device__ __forceinline__ void degrid_mirror_mfma(
     const float *__restrict__ wavenumbers, float2 *__restrict__ visibilities,
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
     const float2 *__restrict__ sg, unsigned *lds) {
-  static_assert(CT % CB == 0, "channel tiles hold whole anchor blocks");
+  static_assert(CT % CB == 0 && CB % 2 == 0,
+                "channel tiles hold whole, even anchor blocks");
   static_assert(KP % 32 == 0, "chunks hold whole K-steps for 4 waves");
   using L = DegridMfmaLds<KP>;
   const int tid = threadIdx.x;
@@ -216,24 +217,29 @@ __device__ __forceinline__ void degrid_mirror_mfma(
     __syncthreads();
   }
 
+  // Chunks of KP pairs are the outermost loop so that building the next
+  // chunk never overlaps live accumulators (no spills); each chunk's partial
+  // sums are added to the visibilities its own lanes wrote for the previous
+  // chunk (same lane, same address: ordered, no atomics).
   const floatx2 inv2pi = {kInv2PiHi, kInv2PiHi};
-  for (int t0 = 0; t0 < nt; t0 += 64) {  // 4 waves x 16 timesteps
-    const int t_row = t0 + wave * 16 + col;  // this lane's A row timestep
-    const idg::UVWCoordinate<float> c = uvw[g.time_offset + min(t_row, nt - 1)];
-    for (int cg0 = 0; cg0 < C; cg0 += CT) {
-      float kk[CT];
+  for (int pc0 = 0; pc0 < half; pc0 += KP) {
+    if (!single) {
+      __syncthreads();
+      build(pc0);
+      __syncthreads();
+    }
+    for (int t0 = 0; t0 < nt; t0 += 64) {  // 4 waves x 16 timesteps
+      const int t_row = t0 + wave * 16 + col;  // this lane's A row timestep
+      const idg::UVWCoordinate<float> c =
+          uvw[g.time_offset + min(t_row, nt - 1)];
+      for (int cg0 = 0; cg0 < C; cg0 += CT) {
+        float kk[CT];
 #pragma unroll
-      for (int j = 0; j < CT; ++j) kk[j] = wavenumbers[min(cg0 + j, C - 1)];
-      floatx4 acc[CT];
+        for (int j = 0; j < CT; ++j) kk[j] = wavenumbers[min(cg0 + j, C - 1)];
+        floatx4 acc[CT];
 #pragma unroll
-      for (int j = 0; j < CT; ++j) acc[j] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-
-      for (int pc0 = 0; pc0 < half; pc0 += KP) {
-        if (!single) {
-          __syncthreads();
-          build(pc0);
-          __syncthreads();
-        }
+        for (int j = 0; j < CT; ++j) acc[j] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        {
         const int nks = (min(KP, half - pc0) + 7) / 8;
         for (int ks = 0; ks < nks; ++ks) {
           const int pp = 8 * ks + 2 * grp;
@@ -259,15 +265,28 @@ __device__ __forceinline__ void degrid_mirror_mfma(
             const floatx2 R =
                 (hi - floatx2{__builtin_rintf(hi.x), __builtin_rintf(hi.y)}) +
                 lo;
+            // Packed over channel pairs (j, j+1) per pixel: the wavenumber
+            // pair is one SGPR pair and pixel terms broadcast, so the phase
+            // is one v_pk_fma per two phasors (same fma(pidx, k, -poff)
+            // rounding as the scalar form).
+            const floatx2 Ax = {A.x, A.x}, Ay = {A.y, A.y};
+            const floatx2 Rx = {R.x, R.x}, Ry = {R.y, R.y};
+            const floatx2 px = {pidx.x, pidx.x}, py = {pidx.y, pidx.y};
+            const floatx2 ox = {npoff.x, npoff.x}, oy = {npoff.y, npoff.y};
 #pragma unroll
-            for (int j = jb; j < jb + CB; ++j) {
-              const floatx2 ph = __builtin_elementwise_fma(
-                  pidx, floatx2{kk[j], kk[j]}, npoff);
-              const floatx2 r = __builtin_elementwise_fma(ph - A, inv2pi, R);
-              float s0, c0, s1, c1;
-              sincos_rev(r.x, &s0, &c0);
-              sincos_rev(r.y, &s1, &c1);
+            for (int j = jb; j < jb + CB; j += 2) {
+              const floatx2 kp = {kk[j], kk[j + 1]};
+              const floatx2 rx = __builtin_elementwise_fma(
+                  __builtin_elementwise_fma(px, kp, ox) - Ax, inv2pi, Rx);
+              const floatx2 ry = __builtin_elementwise_fma(
+                  __builtin_elementwise_fma(py, kp, oy) - Ay, inv2pi, Ry);
+              float s0, c0, s1, c1, s2, c2, s3, c3;
+              sincos_rev(rx.x, &s0, &c0);  // channel j,   pixel 0
+              sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1
+              sincos_rev(rx.y, &s2, &c2);  // channel j+1, pixel 0
+              sincos_rev(ry.y, &s3, &c3);  // channel j+1, pixel 1
               acc[j] = mfma16(split_quad(c0, c1, s0, s1), bf, acc[j]);
+              acc[j + 1] = mfma16(split_quad(c2, c3, s2, s3), bf, acc[j + 1]);
             }
           }
           // one K-step's MFMAs stay in their iteration
@@ -287,11 +306,13 @@ __device__ __forceinline__ void degrid_mirror_mfma(
           if (col < 8 && t < nt && ch < C) {
             float *dst = reinterpret_cast<float *>(
                 visibilities + ((g.time_offset + t) * C + ch) * 4);
-            dst[col] = (v + other) * unscale;
+            const float out = (v + other) * unscale;
+            dst[col] = pc0 == 0 ? out : dst[col] + out;
           }
         }
       }
     }
+  }
   }
 }
 
@@ -334,7 +355,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
     if constexpr (MODE == 1) {
       if (!eligible) return;
       // whole subgrid (S = 32: 512 pairs) in one chunk, else 128-pair chunks
-      constexpr int KP = S_CT == 32 ? 512 : 128;
+      constexpr int KP = 512;
       __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
       degrid_mirror_mfma<S_CT, CT, 16, KP>(g, S, npix, image_size, C,
                                           nr_stations, uvw, wavenumbers,

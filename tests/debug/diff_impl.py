@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.join(REPO, "ska-sdp-idg-bench_amd"))
 import idg_amd
 print("library:", idg_amd.LIB_PATH)
 
-st, ts, T, C, G, S = 50, 20, 128, 16, 1024, 32
+st, ts, T, C, G, S = 50, 20, 128, int(os.environ.get("DIFF_C", 16)), 1024, int(os.environ.get("DIFF_S", 32))
 a = idg_amd.generate(st, ts, T, C, G, S, nthreads=16)
 ns = a["metadata"].size
 dev = {k: torch.from_numpy(a[k]).cuda() for k in ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms", "subgrids")}

@@ -1,0 +1,10 @@
+set -eo pipefail
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 200 python tests/debug/diff_impl.py 2>&1 | grep -v "^  s" 
+DIFF_S=64 timeout -k 10 200 python tests/debug/diff_impl.py 2>&1 | grep -v "^  s"
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.txt 2>&1; tail -2 gpurun_out/pytest_gpu.txt
+for w in default s64 c256; do
+timeout -k 10 300 python bench.py --no-cpu-baseline --workload $w > gpurun_out/b_$w.json 2> gpurun_out/b_$w.err
+python -c "
+import json; d=json.load(open('gpurun_out/b_$w.json')); print('$w', d['value'], d['kernels']['gridder']['ms'], d['kernels']['degridder']['ms'])"
+done
