@@ -47,7 +47,24 @@ WORKLOADS = {
     # configs[4]: large subgrid, A-term + spheroidal
     "s64": dict(nr_stations=50, nr_timeslots=20, nr_timesteps=128,
                 nr_channels=16, grid_size=1024, subgrid_size=64),
+    # the default batch with w-terms -- w ~ U(-200, 200)
+    # per timestep, W_STEP = 2.5 and w-layers z in [0, 7) -- so every
+    # subgrid takes the general (non-mirror) path
+    "wterm": dict(nr_stations=50, nr_timeslots=20, nr_timesteps=128,
+                  nr_channels=16, grid_size=1024, subgrid_size=32,
+                  w_range=200.0, w_step=2.5, w_layers=7),
 }
+
+
+def apply_wterms(w, a):
+    """w-terms of the 'wterm' workload, in place (seeded, numpy)."""
+    import numpy as np
+    if not w.get("w_range"):
+        return
+    rng = np.random.default_rng(7)
+    a["uvw"][..., 2] = rng.uniform(-w["w_range"], w["w_range"],
+                                   a["uvw"].shape[:2])
+    a["metadata"]["z"] = rng.integers(0, w["w_layers"], a["metadata"].size)
 
 
 def parse():
@@ -77,7 +94,8 @@ def cpu_baseline(w, a, nsample):
     n = min(nsample, a["metadata"].size)
     md = a["metadata"][:n]
     T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
-    args = (n, w["grid_size"], S, 0.01, 0.0, C, w["nr_stations"])
+    args = (n, w["grid_size"], S, 0.01, w.get("w_step", 0.0), C,
+            w["nr_stations"])
     if orc.Reference.available(portable=True):
         impl, kind = orc.Reference(portable=True), "reference"
         extra = {}
@@ -151,6 +169,7 @@ def main():
     # ---- synthetic batch (reference generators), resident in HBM ----------
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     a = idg_amd.generate(st, ts, T, C, G, S, nthreads=threads)
+    apply_wterms(w, a)
     idg_amd.validate_metadata(ns, S, C, st, ns * T, ts, a["metadata"])
     dev = {k: torch.from_numpy(a[k]).cuda() for k in
            ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms",
@@ -159,7 +178,8 @@ def main():
         a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
     grid_out = torch.empty_like(dev["subgrids"])
     degrid_out = torch.empty_like(dev["visibilities"])
-    p = (ns, G, S, idg_amd.IMAGE_SIZE, idg_amd.W_STEP, C, st)
+    p = (ns, G, S, idg_amd.IMAGE_SIZE, w.get("w_step", idg_amd.W_STEP), C,
+         st)
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
@@ -258,7 +278,8 @@ def main():
     # exchange step, BASELINE configs[3]), splitter, inverse FFT ----------
     pipeline = None
     if not args.no_pipeline:
-        gridt = torch.zeros((1, 4, G, G, 2), dtype=torch.float32,
+        nw = w.get("w_layers", 1)
+        gridt = torch.zeros((nw, 4, G, G, 2), dtype=torch.float32,
                             device="cuda")
         uvsub = torch.empty_like(grid_out)
         npipe = max(1, min(args.steps, 5))
@@ -275,14 +296,14 @@ def main():
             if e:
                 e[1].record(stream)
             idg_amd.adder_launch(G, dev["metadata"], uvsub, gridt,
-                                 stream=stream)
+                                 nr_w_layers=nw, stream=stream)
             if e:
                 e[2].record(stream)
             dist.reduce_grid(gridt)
             if e:
                 e[3].record(stream)
             idg_amd.splitter_launch(G, dev["metadata"], gridt, uvsub,
-                                    stream=stream)
+                                    nr_w_layers=nw, stream=stream)
             if e:
                 e[4].record(stream)
             idg_amd.subgrid_fft_launch(uvsub, -1, 1.0 / (S * S),
@@ -300,7 +321,8 @@ def main():
             "grid_reduce_ms": round(avg(2, 3), 4),
             "splitter_ms": round(avg(3, 4), 4),
             "ifft_ms": round(avg(4, 5), 4),
-            "grid": f"[1][4][{G}][{G}] complex64, {G * G * 32 / 2**20:.0f} MiB",
+            "grid": (f"[{nw}][4][{G}][{G}] complex64, "
+                     f"{nw * G * G * 32 / 2**20:.0f} MiB"),
             "grid_reduce": ("all_reduce(sum) over RCCL/xGMI" if world > 1
                             else "single rank: no collective"),
         }
@@ -342,10 +364,15 @@ def main():
         "config": {
             "workload": (f"{args.workload}: NR_STATIONS={st} "
                          f"NR_TIMESLOTS={ts} NR_TIMESTEPS_SUBGRID={T} "
-                         f"NR_CHANNELS={C} SUBGRID_SIZE={S} GRID_SIZE={G}"),
+                         f"NR_CHANNELS={C} SUBGRID_SIZE={S} GRID_SIZE={G}"
+                         + (f" W_STEP={w['w_step']} w~U(-{w['w_range']:g},"
+                            f"{w['w_range']:g}) w-layers={w['w_layers']}"
+                            if w.get("w_range") else "")),
             "baseline_config": ("configs[1]" if args.workload == "default"
                                 else {"c256": "configs[2]",
-                                      "s64": "configs[4]"}[args.workload]),
+                                      "s64": "configs[4]",
+                                      "wterm": "SURVEY.md §8f row 4"}[
+                                          args.workload]),
             "nr_subgrids_per_gpu": ns,
             "visibilities_per_gpu_per_step": nvis,
             "step": "gridder + degridder over the batch",

@@ -113,13 +113,15 @@ __device__ __forceinline__ void pixel_entry(
 // ---------------------------------------------------------------------------
 template <int KP>
 struct DegridMfmaLds {
-  static constexpr int kGeoWords = KP * 3;              // l | m | poff
+  static constexpr int kGeoWords = KP * 4;              // l | m | poff | n
   static constexpr int kBfrWords = (KP / 8) * 64 * 2;   // uint2 per lane
-  static constexpr int kWords = kGeoWords + kBfrWords + 8;
+  // 40 KiB at KP = 512: four workgroups per CU (the scale reduction reuses
+  // the start of the geometry area before the first build)
+  static constexpr int kWords = kGeoWords + kBfrWords;
 };
 
-template <int S_CT, int CT, int CB, int KP>
-__device__ __forceinline__ void degrid_mirror_mfma(
+template <int S_CT, int CT, int CB, int KP, bool MIRROR>
+__device__ __forceinline__ void degrid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
     const float *__restrict__ wavenumbers, float2 *__restrict__ visibilities,
@@ -132,7 +134,9 @@ __device__ __forceinline__ void degrid_mirror_mfma(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
-  const int half = npix / 2;
+  // MIRROR: K runs over pixel pairs (b, npix-1-b); general: over single
+  // pixels, as pairs whose mirror term is zero (S = D = P'), w-term on.
+  const int half = MIRROR ? npix / 2 : npix;
   const int nt = g.nr_timesteps;
 
   // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range.
@@ -148,10 +152,11 @@ __device__ __forceinline__ void degrid_mirror_mfma(
   }
   for (int off = 32; off > 0; off >>= 1)
     vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-  float *red = reinterpret_cast<float *>(lds + L::kWords - 8);
+  float *red = reinterpret_cast<float *>(lds);
   if (lane == 0) red[wave] = vmax;
   __syncthreads();
   vmax = 2.0f * fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();  // red[] is geometry space from here on
   int e = 0;
   if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
   const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
@@ -160,6 +165,7 @@ __device__ __forceinline__ void degrid_mirror_mfma(
   float *geo_l = reinterpret_cast<float *>(lds);
   float *geo_m = geo_l + KP;
   float *geo_o = geo_m + KP;
+  float *geo_n = geo_o + KP;
   uint2 *bfr = reinterpret_cast<uint2 *>(lds + L::kGeoWords);
   const bool single = half <= KP;
 
@@ -179,8 +185,12 @@ __device__ __forceinline__ void degrid_mirror_mfma(
           float4 pa, pb, ma, mb, mgeo;
           pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
                       aterms, sg, pa, pb, geo);
-          pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
-                      spheroidal, aterms, sg, ma, mb, mgeo);
+          if constexpr (MIRROR) {
+            pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
+                        spheroidal, aterms, sg, ma, mb, mgeo);
+          } else {
+            ma = mb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          }
           const float pr[4] = {pa.x, pa.z, pb.x, pb.z};
           const float pi[4] = {pa.y, pa.w, pb.y, pb.w};
           const float mr[4] = {ma.x, ma.z, mb.x, mb.z};
@@ -196,6 +206,7 @@ __device__ __forceinline__ void degrid_mirror_mfma(
         geo_l[2 * q + h] = geo.x;
         geo_m[2 * q + h] = geo.y;
         geo_o[2 * q + h] = geo.w;
+        if constexpr (!MIRROR) geo_n[2 * q + h] = geo.z;
       }
       // lane (g, col) of K-step ks: ks = q / 4, g = q % 4
       uint2 *dst = bfr + (q >> 2) * 64 + (q & 3) * 16;
@@ -248,9 +259,14 @@ __device__ __forceinline__ void degrid_mirror_mfma(
           const float2 go = *reinterpret_cast<const float2 *>(geo_o + pp);
           const uint2 bb = bfr[ks * 64 + lane];
           const half8 bf = pack4(bb.x, bb.x, bb.y, bb.y);
-          // phase_index = fma(u, l, v*m) + w*n with w = 0
-          const floatx2 pidx = {fma_(c.u, gl.x, c.v * gm.x),
-                                fma_(c.u, gl.y, c.v * gm.y)};
+          // phase_index = fma(u, l, v*m) + w*n (w = 0 on mirror subgrids)
+          floatx2 pidx = {fma_(c.u, gl.x, c.v * gm.x),
+                          fma_(c.u, gl.y, c.v * gm.y)};
+          if constexpr (!MIRROR) {
+            const float2 gn = *reinterpret_cast<const float2 *>(geo_n + pp);
+            pidx.x = pidx.x + c.w * gn.x;
+            pidx.y = pidx.y + c.w * gn.y;
+          }
           const floatx2 npoff = {-go.x, -go.y};
 #pragma unroll
           for (int jb = 0; jb < CT; jb += CB) {
@@ -319,9 +335,8 @@ __device__ __forceinline__ void degrid_mirror_mfma(
 }  // namespace
 
 // CG: channels per lane (VALU paths).
-// MODE: 0 = VALU kernel (every subgrid), 1 = MFMA kernel (mirror-eligible
-//       subgrids only, others untouched), 2 = fallback of the MFMA kernel
-//       (VALU paths, non-eligible subgrids only; 4 channels per lane).
+// MODE: 0 = VALU kernel, 1 = MFMA kernel (mirror GEMMs on eligible
+//       subgrids, single-pixel GEMMs with the w-term on the others).
 // CT: channels per MFMA pass.
 template <int S_CT, int CG, int MODE, int CT>
 __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
@@ -344,26 +359,34 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
   const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const int C = nr_channels;
 
-  if constexpr (MODE != 0) {
+  if constexpr (MODE == 1) {
+    // chunks of 512 K-pairs (the whole S = 32 subgrid on mirror subgrids)
+    constexpr int KP = 512;
+    __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
     // Subgrid-uniform mirror eligibility: even S, w_offset = 0 and w = 0 on
-    // every timestep (the MFMA kernel and its fallback split on it).
+    // every timestep.  Reduced through lds[0] rather than __syncthreads_or,
+    // whose library implementation adds 256 B of LDS and would cost the
+    // fourth workgroup per CU.
+    if (tid == 0) lds[0] = 0u;
+    __syncthreads();
     bool w_nonzero = false;
     for (int t = tid; t < g.nr_timesteps; t += kBlock)
       w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-    const bool eligible = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
-                          g.w_offset == 0.0f;
-    if constexpr (MODE == 1) {
-      if (!eligible) return;
-      // whole subgrid (S = 32: 512 pairs) in one chunk, else 128-pair chunks
-      constexpr int KP = 512;
-      __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
-      degrid_mirror_mfma<S_CT, CT, 16, KP>(g, S, npix, image_size, C,
+    if (w_nonzero) atomicOr(&lds[0], 1u);
+    __syncthreads();
+    const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
+    __syncthreads();
+    if (eligible)
+      degrid_mfma<S_CT, CT, 16, KP, true>(g, S, npix, image_size, C,
                                           nr_stations, uvw, wavenumbers,
                                           visibilities, spheroidal, aterms,
                                           sg, lds);
-      return;
-    }
-    if (eligible) return;
+    else
+      degrid_mfma<S_CT, CT, 16, KP, false>(g, S, npix, image_size, C,
+                                           nr_stations, uvw, wavenumbers,
+                                           visibilities, spheroidal, aterms,
+                                           sg, lds);
+    return;
   }
 
   // general: [pixel][0..1] = P' (xx, xy | yx, yy), [pixel][2] = (l,m,n,poff)
@@ -371,9 +394,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
   //          [pair][4] = geometry of the base pixel
   __shared__ float4 table[kChunk * 3];
   static_assert(kPairChunk * 5 <= kChunk * 3, "table size");
-  // The fallback of an MFMA build only sees w != 0 / odd-S subgrids: it uses
-  // 4 channels per lane to keep its register budget low.
-  constexpr int CGV = MODE == 2 ? 4 : CG;
+  constexpr int CGV = CG;
   const int ncg = (C + CGV - 1) / CGV;
   const int nunits = g.nr_timesteps * ncg;
   const bool mirror_ok = (S % 2 == 0) && g.w_offset == 0.0f;
@@ -501,9 +522,7 @@ KernelChoice select_degridder(const Problem &p) {
   (s32 ? IDG_DEGRIDDER(32, CG_, MODE_)                                     \
        : (s64 ? IDG_DEGRIDDER(64, CG_, MODE_) : IDG_DEGRIDDER(0, CG_, MODE_)))
   if (mfma) {
-    // the MFMA kernel has no CG; the fallback uses 4 channels per lane
-    k.func = IDG_PICK(4, 1);
-    k.fallback = IDG_PICK(4, 2);
+    k.func = IDG_PICK(4, 1);  // the MFMA kernel has no CG
   } else {
     k.func = cg8 ? IDG_PICK(8, 0) : IDG_PICK(4, 0);
   }

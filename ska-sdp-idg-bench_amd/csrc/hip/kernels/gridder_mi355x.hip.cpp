@@ -12,21 +12,21 @@
 //   phase    = fl(phase_offset(y,x) - phase_index(t,y,x) * k_c)   [one FMA]
 //   subgrid  = sph(y,x) * A1^H P A2
 //
-// Design (DESIGN.md §4.1):
-//  * one workgroup (4 wave64) per subgrid; every visibility is a wave-uniform
-//    operand: uvw, k_c and the 8 floats of V(t,c) are scalar loads (s_load)
-//    feeding the FMAs straight from SGPRs -- no LDS, no vector loads in the
-//    hot loop;
+// Design (DESIGN.md §4):
+//  * one workgroup (4 wave64) per subgrid;
 //  * the fp32 phase is formed exactly as the reference rounds it and reduced
 //    without losing its low bits (device.hpp:revolutions + per-block anchor);
+//  * default (MODE 1): the complex MAC runs on the matrix cores as f16
+//    two-term-split GEMMs (v_mfma_f32_16x16x32_f16, grid_mfma below), pixels
+//    x (timestep, channel) x correlation components;
 //  * mirror pixels: for even S, pixel (y,x) and (S-1-y, S-1-x) have exactly
 //    negated l, m; when w = 0 and the subgrid's w_offset = 0 (every benchmark
 //    configuration) their reference phases are exact negatives (fma rounding
 //    is sign-symmetric), so one range reduction and one v_sin/v_cos pair
-//    serve both pixels: P_p += V*(c, s), P_mirror += V*(c, -s).  Subgrids
-//    with any w != 0 take the general per-pixel path;
-//  * 4 correlations x complex MAC = 16 FMAs per (pixel, t, c), packed by the
-//    compiler into v_pk_fma_f32 (2 FMAs per lane per issue on gfx950).
+//    serve both pixels.  Subgrids with any w != 0 (or odd S) run the same
+//    GEMMs over every pixel with the w-term in the phase;
+//  * IDG_GRIDDER_IMPL=valu (MODE 0) selects the all-VALU kernel: 16 FMAs per
+//    (pixel, t, c) with wave-uniform visibilities in SGPRs (A/B reference).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -209,8 +209,8 @@ struct MfmaLds {
       (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
 };
 
-template <int S_CT, int PT, int CB>
-__device__ __forceinline__ void grid_mirror_mfma(
+template <int S_CT, int PT, int CB, bool MIRROR>
+__device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
     const float *__restrict__ wavenumbers,
@@ -221,7 +221,9 @@ __device__ __forceinline__ void grid_mirror_mfma(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
-  const int half = npix / 2;
+  // MIRROR: base pixels b < npix/2 (mirror npix-1-b shares the phasor);
+  // general: every pixel is a base pixel and Y is added, not mirrored.
+  const int half = MIRROR ? npix / 2 : npix;
   const int nt = g.nr_timesteps;
   const int nchq = (C + 3) / 4;  // channel quads
 
@@ -256,13 +258,13 @@ __device__ __forceinline__ void grid_mirror_mfma(
   const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
 
   for (int gbase = 0; gbase < half; gbase += 64 * PT) {
-    float lg[PT], mg[PT];
+    float lg[PT], mg[PT], ng[PT];
     floatx2 pg2[PT];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
-      float n_unused, pg;
-      pixel_geometry(b, S, image_size, g, lg[i], mg[i], n_unused, pg);
+      float pg;
+      pixel_geometry(b, S, image_size, g, lg[i], mg[i], ng[i], pg);
       pg2[i] = floatx2{pg, pg};
     }
     floatx4 accx[PT], accy[PT];
@@ -332,7 +334,11 @@ __device__ __forceinline__ void grid_mirror_mfma(
           floatx2 np2[PT];
 #pragma unroll
           for (int i = 0; i < PT; ++i) {
-            const float pidx = fma_(c.u, lg[i], c.v * mg[i]);
+            // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
+            // subgrids, where fma(0, n, x) == x
+            const float pidx =
+                MIRROR ? fma_(c.u, lg[i], c.v * mg[i])
+                       : fma_(c.w, ng[i], fma_(c.u, lg[i], c.v * mg[i]));
             np2[i] = floatx2{-pidx, -pidx};
           }
           for (int jb = 0; jb < nj; jb += CB / 4) {
@@ -435,15 +441,17 @@ __device__ __forceinline__ void grid_mirror_mfma(
       const float y[8] = {yh0.x + yl0.x, yh0.y + yl0.y, yh0.z + yl0.z,
                           yh0.w + yl0.w, yh1.x + yl1.x, yh1.y + yl1.y,
                           yh1.z + yl1.z, yh1.w + yl1.w};
-      float ab[8], am[8];
+      float ab[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ab[j] = (x[j] + y[j]) * unscale;
-        am[j] = (x[j] - y[j]) * unscale;
-      }
+      for (int j = 0; j < 8; ++j) ab[j] = (x[j] + y[j]) * unscale;
       store_pixel(ab, b, S, npix, g, nr_stations, spheroidal, aterms, out);
-      store_pixel(am, npix - 1 - b, S, npix, g, nr_stations, spheroidal,
-                  aterms, out);
+      if constexpr (MIRROR) {
+        float am[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) am[j] = (x[j] - y[j]) * unscale;
+        store_pixel(am, npix - 1 - b, S, npix, g, nr_stations, spheroidal,
+                    aterms, out);
+      }
     }
     __syncthreads();
   }
@@ -454,8 +462,8 @@ __device__ __forceinline__ void grid_mirror_mfma(
 // S_CT: subgrid size known at compile time (0 = runtime).
 // PPT : pixels per lane (VALU paths).   CB: channels per phase anchor.
 // MODE: 0 = VALU kernel (VALU mirror path + general path, every subgrid),
-//       1 = MFMA kernel (mirror-eligible subgrids only, others untouched),
-//       2 = fallback of the MFMA kernel (general path, non-eligible only).
+//       1 = MFMA kernel (mirror path on eligible subgrids, the same GEMMs
+//           over every pixel with the w-term on the others).
 // PT  : 16-pixel base tiles per wave in the MFMA path.
 template <int S_CT, int PPT, int CB, int MODE, int PT>
 __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
@@ -489,16 +497,19 @@ __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
                       g.w_offset == 0.0f;
 
   if constexpr (MODE == 1) {
-    if (!mirror) return;
     __shared__ unsigned lds[MfmaLds<PT>::kWords];
-    grid_mirror_mfma<S_CT, PT, CB>(g, S, npix, image_size, C, nr_stations,
-                                   uvw, wavenumbers, visibilities, spheroidal,
-                                   aterms, out, lds);
+    if (mirror)
+      grid_mfma<S_CT, PT, CB, true>(g, S, npix, image_size, C, nr_stations,
+                                    uvw, wavenumbers, visibilities,
+                                    spheroidal, aterms, out, lds);
+    else
+      grid_mfma<S_CT, PT, CB, false>(g, S, npix, image_size, C, nr_stations,
+                                     uvw, wavenumbers, visibilities,
+                                     spheroidal, aterms, out, lds);
     return;
   }
-  if (MODE == 2 && mirror) return;
 
-  if (MODE == 0 && mirror) {
+  if (mirror) {
     // Mirror-pair path: lane owns base pixels b (< npix/2) and npix-1-b.
     const int half = npix / 2;
     for (int tile = 0; tile < half; tile += kBlock * NB) {
@@ -581,17 +592,14 @@ KernelChoice select_gridder(const Problem &p) {
   switch (p.subgrid_size) {
     case 32:
       k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
-      k.fallback = mfma ? IDG_GRIDDER(32, 4, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
       break;
     case 64:
       k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);
-      k.fallback = mfma ? IDG_GRIDDER(64, 4, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_s64" : "gridder_mi355x_s64_valu";
       break;
     default:
       k.func = mfma ? IDG_GRIDDER(0, 2, 1) : IDG_GRIDDER(0, 2, 0);
-      k.fallback = mfma ? IDG_GRIDDER(0, 2, 2) : nullptr;
       k.name = mfma ? "gridder_mi355x_generic" : "gridder_mi355x_generic_valu";
       break;
   }

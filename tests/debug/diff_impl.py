@@ -10,10 +10,16 @@ print("library:", idg_amd.LIB_PATH)
 
 st, ts, T, C, G, S = 50, 20, 128, int(os.environ.get("DIFF_C", 16)), 1024, int(os.environ.get("DIFF_S", 32))
 a = idg_amd.generate(st, ts, T, C, G, S, nthreads=16)
+WSTEP = 0.0
+if os.environ.get("DIFF_W"):  # w-terms as bench.py's 'wterm' workload
+    rng = np.random.default_rng(7)
+    a["uvw"][..., 2] = rng.uniform(-200.0, 200.0, a["uvw"].shape[:2])
+    a["metadata"]["z"] = rng.integers(0, 7, a["metadata"].size)
+    WSTEP = 2.5
 ns = a["metadata"].size
 dev = {k: torch.from_numpy(a[k]).cuda() for k in ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms", "subgrids")}
 md = torch.from_numpy(a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
-p = (ns, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st)
+p = (ns, G, S, idg_amd.IMAGE_SIZE, WSTEP, C, st)
 out = {}
 for impl in ("valu", "mfma"):
     os.environ["IDG_GRIDDER_IMPL"] = impl

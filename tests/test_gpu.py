@@ -106,6 +106,8 @@ SWEEP = [
     (2, 1, 33, 12, 1024, 32),   # C = 12 (channel group of 4)
     (2, 1, 4, 300, 1024, 32),   # many channels (several anchor blocks)
     (2, 1, 700, 2, 1024, 32),   # many timesteps (> 256 degridder units)
+    (2, 1, 7, 3, 256, 33),      # odd S: no mirror pairs, single-pixel GEMMs
+    (2, 1, 6, 5, 128, 15),      # odd S, S^2 = 225 < one 256-pixel pass
 ]
 
 
@@ -130,9 +132,19 @@ def test_geometry_sweep_vs_oracle(idg, oracle_lib, geom):
     assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
 
 
-def test_w_terms_vs_oracle(idg, oracle_lib):
+W_SWEEP = [
+    (3, 2, 16, 8, 512, 32),
+    (2, 1, 9, 7, 256, 24),
+    (2, 1, 5, 3, 256, 33),      # odd S
+    (2, 1, 3, 5, 1024, 64),     # S = 64: several K-chunks per subgrid
+    (2, 1, 4, 300, 1024, 32),   # many channels
+]
+
+
+@pytest.mark.parametrize("geom", W_SWEEP)
+def test_w_terms_vs_oracle(idg, oracle_lib, geom):
     # non-zero w and w_step exercise the n-term fusion (row a3 of §8)
-    st, ts, T, C, G, S = 3, 2, 16, 8, 512, 32
+    st, ts, T, C, G, S = geom
     a = idg.generate(st, ts, T, C, G, S)
     rng = np.random.default_rng(3)
     a["uvw"][..., 2] = rng.uniform(-200, 200, a["uvw"].shape[:2])
@@ -147,6 +159,30 @@ def test_w_terms_vs_oracle(idg, oracle_lib):
                        a["visibilities"], a["spheroidal"], a["aterms"], md, go)
     assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
     d = _degrid(idg, p, a, md=md)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], md, a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+def test_mixed_mirror_and_general_subgrids_in_one_launch(idg, oracle_lib):
+    # w = 0 subgrids (mirror GEMMs) next to w != 0 subgrids (single-pixel
+    # GEMMs) in the same launch; W_STEP = 0 so only w decides
+    st, ts, T, C, G, S = 4, 2, 16, 8, 512, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    md = a["metadata"]
+    rng = np.random.default_rng(5)
+    # uvw is [baselines][T]; subgrid s covers row s: w on every third one
+    a["uvw"][1::3, :, 2] = rng.uniform(-150, 150, a["uvw"][1::3, :, 2].shape)
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    g = _grid(idg, p, a)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"], md, go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a)
     do = np.zeros_like(d)
     oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
                          a["spheroidal"], a["aterms"], md, a["subgrids"])
@@ -216,11 +252,32 @@ def full(idg):
     p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
              subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
              nr_channels=C, nr_stations=st)
+    return p, a, _to_device(a)
+
+
+def _to_device(a):
+    import torch
     dev = {k: torch.from_numpy(v).cuda() for k, v in a.items()
            if k not in ("metadata", "frequencies")}
     dev["metadata"] = torch.from_numpy(
         a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
-    return p, a, dev
+    return dev
+
+
+@pytest.fixture(scope="module")
+def full_w(idg):
+    """configs[1] sizes with w-terms (bench.py
+    workload 'wterm'): w ~ U(-200, 200), W_STEP = 2.5, w-layers z in [0, 7),
+    so every subgrid takes the general (non-mirror) GEMM path."""
+    st, ts, T, C, G, S = 50, 20, 128, 16, 1024, 32
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    rng = np.random.default_rng(7)
+    a["uvw"][..., 2] = rng.uniform(-200.0, 200.0, a["uvw"].shape[:2])
+    a["metadata"]["z"] = rng.integers(0, 7, a["metadata"].size)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=2.5,
+             nr_channels=C, nr_stations=st)
+    return p, a, _to_device(a)
 
 
 def _dgrid(idg, p, dev, vis, md=None):
@@ -243,8 +300,15 @@ def _ddegrid(idg, p, dev, sg):
 
 
 def test_full_size_sampled_subgrids_vs_oracle(idg, oracle_lib, full):
+    _sampled_vs_oracle(idg, oracle_lib, *full)
+
+
+def test_full_size_wterm_sampled_subgrids_vs_oracle(idg, oracle_lib, full_w):
+    _sampled_vs_oracle(idg, oracle_lib, *full_w)
+
+
+def _sampled_vs_oracle(idg, oracle_lib, p, a, dev):
     import torch
-    p, a, dev = full
     g = _dgrid(idg, p, dev, dev["visibilities"]).cpu().numpy()
     d = _ddegrid(idg, p, dev, dev["subgrids"]).cpu().numpy()
     torch.cuda.synchronize()
@@ -270,14 +334,17 @@ def test_full_size_sampled_subgrids_vs_oracle(idg, oracle_lib, full):
 
 
 @pytest.mark.parametrize("op", ["gridder", "degridder"])
-def test_full_size_mfma_path_matches_valu_path_every_subgrid(idg, full, op,
-                                                              monkeypatch):
+@pytest.mark.parametrize("data", ["w0", "wterm"])
+def test_full_size_mfma_path_matches_valu_path_every_subgrid(
+        idg, full, full_w, op, data, monkeypatch):
     """The f16-split MFMA kernels against the all-f32 VALU kernels on EVERY
     subgrid of the full config, twice (run-to-run bitwise identical).  This
     is the check that caught a schedule-dependent accumulator corruption in
-    ~5 % of subgrids which the sampled oracle comparison only hit by luck."""
+    ~5 % of subgrids which the sampled oracle comparison only hit by luck.
+    'w0': the benchmark data (mirror GEMMs); 'wterm': w != 0 everywhere
+    (single-pixel GEMMs with the w-term)."""
     import torch
-    p, a, dev = full
+    p, a, dev = full if data == "w0" else full_w
     env = "IDG_GRIDDER_IMPL" if op == "gridder" else "IDG_DEGRIDDER_IMPL"
     run = ((lambda: _dgrid(idg, p, dev, dev["visibilities"]))
            if op == "gridder" else
