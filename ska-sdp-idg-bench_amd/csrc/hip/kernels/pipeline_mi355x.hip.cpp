@@ -109,31 +109,109 @@ __global__ void __launch_bounds__(256)
 }
 
 // grid[z][pol][cy + y][cx + x] += shift_phasor(x, y) * F[s][pol][ys][xs],
-// ys = (y + S/2) % S, xs = (x + S/2) % S.  Overlapping subgrids meet in
-// float atomics (order, hence the last bits, not deterministic).
+// ys = (y + S/2) % S, xs = (x + S/2) % S.
+//
+// A gather, not a scatter: one workgroup owns one 32 x 32 tile of one
+// w-layer, finds the subgrids that overlap it (an ordered scan of the
+// metadata: ballot + prefix per 256-subgrid chunk into an LDS list), adds
+// their pixels into registers in subgrid order and read-modify-writes the
+// tile once.  Every subgrid pixel is read exactly once over the whole
+// launch, there are no atomics, and the summation order -- hence every bit
+// of the grid -- is deterministic.
+constexpr int kAddTile = 32;      // grid tile edge (pixels)
+constexpr int kAddPix = 4;        // tile pixels per thread (1024 / 256)
+constexpr int kAddMaxTable = 256; // shift phasors kept in LDS for S <= 128
+static_assert(kAddTile * kAddTile == 256 * kAddPix, "tile = block x pixels");
+
 __global__ void __launch_bounds__(256)
-    kernel_adder(const idg::Metadata *__restrict__ metadata,
+    kernel_adder(const idg::Metadata *__restrict__ metadata, int nr_subgrids,
                  const float2 *__restrict__ subgrids,
                  float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
-  const int s = blockIdx.x;
-  const idg::Metadata m = metadata[s];
-  if (!fits(m, G, S, nr_w_layers)) return;
+  __shared__ int list[256];
+  __shared__ int2 corner[256];
+  __shared__ int wave_count[4];
+  __shared__ float2 table[kAddMaxTable];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntx = (G + kAddTile - 1) / kAddTile;
+  const int tx0 = (blockIdx.x % ntx) * kAddTile;
+  const int ty0 = (blockIdx.x / ntx) * kAddTile;
+  const int z = blockIdx.y;
   const int npix = S * S;
-  const float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
-  float *g = reinterpret_cast<float *>(
-      grid + static_cast<size_t>(m.coordinate.z) * 4 * G * G);
-  for (int i = threadIdx.x; i < npix; i += blockDim.x) {
-    const int y = i / S, x = i - y * S;
-    const int src = ((y + S / 2) % S) * S + (x + S / 2) % S;
-    const float2 ph = shift_phasor(x, y, S, 1.0f);
-    const size_t dst =
-        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+  const bool tabled = 2 * S - 1 <= kAddMaxTable;
+  // shift phasor depends on x + y only
+  if (tabled)
+    for (int k = tid; k < 2 * S - 1; k += 256)
+      table[k] = unit_phasor(k * (S + 1) - S, 2 * S, 1.0f);
+
+  float2 acc[kAddPix][4];
+#pragma unroll
+  for (int j = 0; j < kAddPix; ++j)
+#pragma unroll
+    for (int pol = 0; pol < 4; ++pol) acc[j][pol] = make_float2(0.0f, 0.0f);
+
+  for (int base = 0; base < nr_subgrids; base += 256) {
+    const int s = base + tid;
+    bool hit = false;
+    int cx = 0, cy = 0;
+    if (s < nr_subgrids) {
+      const idg::Metadata m = metadata[s];
+      cx = m.coordinate.x;
+      cy = m.coordinate.y;
+      hit = fits(m, G, S, nr_w_layers) && m.coordinate.z == z &&
+            cx < tx0 + kAddTile && cx + S > tx0 && cy < ty0 + kAddTile &&
+            cy + S > ty0;
+    }
+    const unsigned long long mask = __ballot(hit);
+    __syncthreads();  // the previous chunk's list is consumed
+    if (lane == 0) wave_count[wave] = __popcll(mask);
+    __syncthreads();
+    int offset = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      offset += w < wave ? wave_count[w] : 0;
+      total += wave_count[w];
+    }
+    if (hit) {
+      const int pos =
+          offset + __popcll(mask & ((1ull << lane) - 1ull));  // ordered
+      list[pos] = s;
+      corner[pos] = make_int2(cx, cy);
+    }
+    __syncthreads();
+    for (int e = 0; e < total; ++e) {
+      const int2 c = corner[e];
+      const float2 *sg = subgrids + static_cast<size_t>(list[e]) * 4 * npix;
+#pragma unroll
+      for (int j = 0; j < kAddPix; ++j) {
+        const int i = tid + 256 * j;
+        const int x = tx0 + (i & (kAddTile - 1)) - c.x;
+        const int y = ty0 + i / kAddTile - c.y;
+        if (x < 0 || x >= S || y < 0 || y >= S) continue;
+        const int src = ((y + S / 2) % S) * S + (x + S / 2) % S;
+        const float2 ph =
+            tabled ? table[x + y] : shift_phasor(x, y, S, 1.0f);
+#pragma unroll
+        for (int pol = 0; pol < 4; ++pol) {
+          const float2 v = cmulf(ph, sg[pol * npix + src]);
+          acc[j][pol].x += v.x;
+          acc[j][pol].y += v.y;
+        }
+      }
+    }
+  }
+
+  float2 *gz = grid + static_cast<size_t>(z) * 4 * G * G;
+#pragma unroll
+  for (int j = 0; j < kAddPix; ++j) {
+    const int i = tid + 256 * j;
+    const int gx = tx0 + (i & (kAddTile - 1)), gy = ty0 + i / kAddTile;
+    if (gx >= G || gy >= G) continue;
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol) {
-      const float2 v = cmulf(ph, sg[pol * npix + src]);
-      const size_t o = 2 * (static_cast<size_t>(pol) * G * G + dst);
-      unsafeAtomicAdd(g + o, v.x);
-      unsafeAtomicAdd(g + o + 1, v.y);
+      float2 *o = gz + static_cast<size_t>(pol) * G * G +
+                  static_cast<size_t>(gy) * G + gx;
+      const float2 v = *o;
+      *o = make_float2(v.x + acc[j][pol].x, v.y + acc[j][pol].y);
     }
   }
 }
@@ -250,10 +328,12 @@ hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
                         int nr_w_layers, const void *d_metadata,
                         const void *d_subgrids, void *d_grid,
                         hipStream_t stream) {
-  if (nr_subgrids <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kernel_adder, dim3(nr_subgrids), dim3(256), 0, stream,
-                     static_cast<const idg::Metadata *>(d_metadata),
-                     static_cast<const float2 *>(d_subgrids),
+  if (nr_subgrids <= 0 || nr_w_layers <= 0 || grid_size <= 0)
+    return hipSuccess;
+  const int ntx = (grid_size + kAddTile - 1) / kAddTile;
+  hipLaunchKernelGGL(kernel_adder, dim3(ntx * ntx, nr_w_layers), dim3(256), 0,
+                     stream, static_cast<const idg::Metadata *>(d_metadata),
+                     nr_subgrids, static_cast<const float2 *>(d_subgrids),
                      static_cast<float2 *>(d_grid), grid_size, subgrid_size,
                      nr_w_layers);
   return hipGetLastError();

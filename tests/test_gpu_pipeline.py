@@ -53,7 +53,8 @@ def _random_case(rng, G, S, W, ns):
     return md, sub
 
 
-@pytest.mark.parametrize("S,G,W", [(32, 128, 1), (16, 96, 3), (64, 160, 2)])
+@pytest.mark.parametrize("S,G,W", [(32, 128, 1), (16, 96, 3), (64, 160, 2),
+                                   (24, 100, 2), (14, 70, 1), (136, 300, 1)])
 def test_adder_matches_numpy(idg, S, G, W):
     import torch
     rng = np.random.default_rng(S * G)
@@ -140,3 +141,10 @@ def test_full_size_adder_sampled_vs_numpy(idg):
     assert _rel(got, ref) < 1e-5
     fits = ((a["metadata"]["x"] + S <= G) & (a["metadata"]["y"] + S <= G))
     assert 0 < fits.sum() < ns       # some subgrids fall off the grid edge
+
+    # the gather adder is deterministic: a second pass onto the same grid
+    # adds the identical per-tile sums, so the grid is exactly doubled
+    once = grid.clone()
+    idg.adder_launch(G, md, sub, grid)
+    torch.cuda.synchronize()
+    assert torch.equal(grid, 2 * once)
