@@ -178,7 +178,8 @@ int idg_subgrid_fft_launch(int nr_subgrids, int subgrid_size, int sign,
 
 /* grid[z][pol][y0 + y][x0 + x] += exp(i pi ((x + y)(S + 1)/S - 1)) *
  * subgrid[s][pol][(y + S/2) % S][(x + S/2) % S]; subgrids not wholly inside
- * the grid are skipped.  Float atomics: summation order not deterministic. */
+ * the grid are skipped.  Deterministic: a per-tile gather in subgrid order,
+ * no atomics. */
 int idg_adder_launch(int nr_subgrids, int grid_size, int subgrid_size,
                      int nr_w_layers, const idg_metadata_t *metadata,
                      const idg_cfloat_t *subgrids, idg_cfloat_t *grid,
