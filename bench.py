@@ -323,8 +323,8 @@ def main():
             "ifft_ms": round(avg(4, 5), 4),
             "grid": (f"[{nw}][4][{G}][{G}] complex64, "
                      f"{nw * G * G * 32 / 2**20:.0f} MiB"),
-            "grid_reduce": ("all_reduce(sum) over RCCL/xGMI" if world > 1
-                            else "single rank: no collective"),
+            "grid_reduce": (f"all_reduce(sum), {dist.backend_name()}"
+                            if world > 1 else "single rank: no collective"),
         }
         extra = sum(pipeline[k] for k in ("fft_ms", "adder_ms",
                                           "grid_reduce_ms", "splitter_ms",

@@ -6,6 +6,8 @@ barrier / max-over-ranks timing, optional gathers of shard outputs, and the
 one real exchange step of the pipeline: summing the ranks' partial uv grids
 (reduce_grid, SURVEY.md §8e "final grid-sum").
 Backend "nccl" is RCCL on ROCm (over xGMI); "gloo" runs the same code on CPU.
+IDG_DIST_BACKEND=gloo forces gloo with GPUs present, so a multi-rank run can be
+rehearsed with several ranks sharing one device (RCCL refuses that).
 """
 import os
 
@@ -23,9 +25,13 @@ def init(backend=None):
     """Initialise the process group when WORLD_SIZE > 1.  Returns
     (rank, local_rank, world_size)."""
     rank, local_rank, world = env_rank()
+    if torch.cuda.is_available():
+        # more ranks than devices only in a gloo rehearsal (IDG_DIST_BACKEND)
+        local_rank %= max(1, torch.cuda.device_count())
     if world > 1 and not torch_dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("IDG_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
@@ -37,6 +43,14 @@ def init(backend=None):
     elif torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
     return rank, local_rank, world
+
+
+def backend_name():
+    """What the collectives run on, for reports."""
+    if not torch_dist.is_initialized():
+        return "none"
+    b = torch_dist.get_backend()
+    return "RCCL over xGMI" if b == "nccl" else b
 
 
 def _device():
