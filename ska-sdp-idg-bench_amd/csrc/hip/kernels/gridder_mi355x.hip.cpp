@@ -44,6 +44,10 @@
 #ifndef IDG_GRID_WAVES
 #define IDG_GRID_WAVES 4
 #endif
+// waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
+#ifndef IDG_GRID_NW
+#define IDG_GRID_NW 8
+#endif
 
 namespace idg_mi355x {
 
@@ -201,15 +205,17 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 // ---------------------------------------------------------------------------
 constexpr int kKsBuf = 16;  // K-steps (16 items each) of B fragments per fill
 
-template <int PT>
+// NW waves per workgroup, PT 16-pixel tiles per wave: NW * 16 * PT base
+// pixels per pass, and each B fragment is built once per pass.
+template <int PT, int NW>
 struct MfmaLds {
-  static constexpr int kObufFloats = 2 * 64 * PT * 16;  // X and Y tiles
-  static constexpr int kBbufWords = kKsBuf * 64 * 8;    // uint4 X + uint4 Y
+  static constexpr int kObufFloats = 2 * NW * 16 * PT * 16;  // X and Y tiles
+  static constexpr int kBbufWords = kKsBuf * 64 * 8;  // uint4 X + uint4 Y
   static constexpr int kWords =
       (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
 };
 
-template <int S_CT, int PT, int CB, bool MIRROR>
+template <int S_CT, int PT, int CB, int NW, bool MIRROR>
 __device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -233,17 +239,18 @@ __device__ __forceinline__ void grid_mfma(
     const float4 *v4 = reinterpret_cast<const float4 *>(
         visibilities + g.time_offset * C * 4);
     const int n4 = nt * C * 2;
-    for (int i = tid; i < n4; i += kBlock) {
+    for (int i = tid; i < n4; i += NW * 64) {
       const float4 q = v4[i];
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)),
                                fmaxf(fabsf(q.z), fabsf(q.w))));
     }
     for (int off = 32; off > 0; off >>= 1)
       vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT>::kWords - 8);
+    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT, NW>::kWords - 8);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();
-    vmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+#pragma unroll
+    for (int w = 0; w < NW; ++w) vmax = fmaxf(vmax, red[w]);
   }
   int e = 0;
   if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
@@ -257,7 +264,8 @@ __device__ __forceinline__ void grid_mfma(
   const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
   const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
 
-  for (int gbase = 0; gbase < half; gbase += 64 * PT) {
+  constexpr int kPass = NW * 16 * PT;  // base pixels per pass
+  for (int gbase = 0; gbase < half; gbase += kPass) {
     float lg[PT], mg[PT], ng[PT];
     floatx2 pg2[PT];
 #pragma unroll
@@ -293,7 +301,7 @@ __device__ __forceinline__ void grid_mfma(
           const float bpart = (col & 8) ? -1.0f : 0.0f;
           const int nks = nq * nj;
           const bool full = (q0 + nq) * 4 <= nt && 4 * (j0 + nj) <= C;
-          for (int ks = wave; ks < nks; ks += kBlock / 64) {
+          for (int ks = wave; ks < nks; ks += NW) {
             const int qq = ks / nj, jj = ks - qq * nj;
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
@@ -421,18 +429,18 @@ __device__ __forceinline__ void grid_mfma(
       for (int r = 0; r < 4; ++r) {
         const int lp = (wave * PT + i) * 16 + grp * 4 + r;
         obuf[lp * 16 + col] = accx[i][r];
-        obuf[(64 * PT + lp) * 16 + col] = accy[i][r];
+        obuf[(kPass + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
 #ifdef IDG_DBG_NOEPI
     if (gbase >= 0) { __syncthreads(); continue; }
 #endif
-    for (int q = tid; q < 64 * PT; q += kBlock) {
+    for (int q = tid; q < kPass; q += NW * 64) {
       const int b = gbase + q;
       if (b >= half) continue;
       const float4 *xr = reinterpret_cast<const float4 *>(obuf + q * 16);
       const float4 *yr =
-          reinterpret_cast<const float4 *>(obuf + (64 * PT + q) * 16);
+          reinterpret_cast<const float4 *>(obuf + (kPass + q) * 16);
       const float4 xh0 = xr[0], xh1 = xr[1], xl0 = xr[2], xl1 = xr[3];
       const float4 yh0 = yr[0], yh1 = yr[1], yl0 = yr[2], yl1 = yr[3];
       const float x[8] = {xh0.x + xl0.x, xh0.y + xl0.y, xh0.z + xl0.z,
@@ -466,7 +474,8 @@ __device__ __forceinline__ void grid_mfma(
 //           over every pixel with the w-term on the others).
 // PT  : 16-pixel base tiles per wave in the MFMA path.
 template <int S_CT, int PPT, int CB, int MODE, int PT>
-__global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
+__global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
+                                  IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
                           float image_size, float w_step_in_lambda,
                           int nr_channels, int nr_stations,
@@ -491,21 +500,24 @@ __global__ void __launch_bounds__(kBlock, IDG_GRID_WAVES)
   // Mirror pairs need w = 0 on every timestep of the subgrid (checked once,
   // so the two paths below stay separate loops with separate registers).
   bool w_nonzero = false;
-  for (int t = tid; t < g.nr_timesteps; t += kBlock)
+  for (int t = tid; t < g.nr_timesteps; t += blockDim.x)
     w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
   const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
                       g.w_offset == 0.0f;
 
   if constexpr (MODE == 1) {
-    __shared__ unsigned lds[MfmaLds<PT>::kWords];
+    constexpr int NW = IDG_GRID_NW;
+    __shared__ unsigned lds[MfmaLds<PT, NW>::kWords];
     if (mirror)
-      grid_mfma<S_CT, PT, CB, true>(g, S, npix, image_size, C, nr_stations,
-                                    uvw, wavenumbers, visibilities,
-                                    spheroidal, aterms, out, lds);
+      grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
+                                        nr_stations, uvw, wavenumbers,
+                                        visibilities, spheroidal, aterms, out,
+                                        lds);
     else
-      grid_mfma<S_CT, PT, CB, false>(g, S, npix, image_size, C, nr_stations,
-                                     uvw, wavenumbers, visibilities,
-                                     spheroidal, aterms, out, lds);
+      grid_mfma<S_CT, PT, CB, NW, false>(g, S, npix, image_size, C,
+                                         nr_stations, uvw, wavenumbers,
+                                         visibilities, spheroidal, aterms,
+                                         out, lds);
     return;
   }
 
@@ -587,8 +599,8 @@ static int gridder_impl() {
 KernelChoice select_gridder(const Problem &p) {
   KernelChoice k;
   k.grid = p.nr_subgrids;
-  k.block = kBlock;
   const bool mfma = gridder_impl() == 1;
+  k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
   switch (p.subgrid_size) {
     case 32:
       k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
