@@ -288,43 +288,43 @@ __device__ __forceinline__ void grid_mfma(
         const int nj = min(cq_per_fill, nchq - j0);
         // ---- B fragments for nq timestep quads x nj channel quads -> LDS.
         // One wave fills one K-step (lane = group g, column col): items
-        // (t = 4q+g, c0..c0+3), each a float2 load of the column's
-        // correlation; bc/bs formed with the lane's (re, im) selectors,
-        // then split to the column's f16 part.
+        // (t = 4q+g, c0..c0+3), two word loads each, scaled, then split to
+        // the column's f16 part.
         __syncthreads();
         {
-          // this lane's B column: correlation, (re | im) selectors with the
-          // scale folded in, and which f16 part (hi: 0, lo: -1) it holds
+          // this lane's B column: correlation bpol, re (even col) or im
+          // (odd col) part, and which f16 part (hi: 0, lo: -1) it holds.
+          // Column re: bc = re, bs = -im;  column im: bc = im, bs = re --
+          // so the lane loads exactly the two words it needs and only
+          // scales them (the sign of bs folded into its scale).
           const int bpol = (col & 7) >> 1;
-          const float sel_re = (col & 1) ? 0.0f : scale;
-          const float sel_im = (col & 1) ? scale : 0.0f;
+          const int w_c = 2 * bpol + (col & 1);        // word of bc
+          const int w_s = 2 * bpol + 1 - (col & 1);    // word of bs
+          const float sc_s = (col & 1) ? scale : -scale;
           const float bpart = (col & 8) ? -1.0f : 0.0f;
+          const float *vsubf = reinterpret_cast<const float *>(vsub);
           const int nks = nq * nj;
           const bool full = (q0 + nq) * 4 <= nt && 4 * (j0 + nj) <= C;
           for (int ks = wave; ks < nks; ks += NW) {
             const int qq = ks / nj, jj = ks - qq * nj;
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
-            float2 b[4];
+            float bc[4], bs[4];
             if (full) {
-              const float2 *src = vsub + (t * C + c0) * 4 + bpol;
+              const float *src = vsubf + (t * C + c0) * 8;
 #pragma unroll
-              for (int u = 0; u < 4; ++u) b[u] = src[4 * u];
+              for (int u = 0; u < 4; ++u) {
+                bc[u] = src[8 * u + w_c] * scale;
+                bs[u] = src[8 * u + w_s] * sc_s;
+              }
             } else {
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
                 const bool ok = t < nt && c0 + u < C;
                 const int it = ok ? t * C + c0 + u : 0;
-                const float2 v = vsub[it * 4 + bpol];
-                b[u] = ok ? v : make_float2(0.0f, 0.0f);
+                bc[u] = ok ? vsubf[it * 8 + w_c] * scale : 0.0f;
+                bs[u] = ok ? vsubf[it * 8 + w_s] * sc_s : 0.0f;
               }
-            }
-            float bc[4], bs[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              // column (re): bc = re, bs = -im;  column (im): bc = im, bs = re
-              bc[u] = fma_(b[u].y, sel_im, b[u].x * sel_re);
-              bs[u] = fma_(b[u].x, sel_im, -(b[u].y * sel_re));
             }
             const unsigned xc = split_part(bc[0], bc[1], bpart);
             const unsigned yc = split_part(bc[2], bc[3], bpart);
