@@ -432,9 +432,6 @@ __device__ __forceinline__ void grid_mfma(
         obuf[(kPass + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
-#ifdef IDG_DBG_NOEPI
-    if (gbase >= 0) { __syncthreads(); continue; }
-#endif
     for (int q = tid; q < kPass; q += NW * 64) {
       const int b = gbase + q;
       if (b >= half) continue;

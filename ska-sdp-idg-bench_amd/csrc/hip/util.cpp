@@ -252,12 +252,8 @@ hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
                   &d_uvw,         &d_wavenumbers,   &d_visibilities,
                   &d_spheroidal,  &d_aterms,        &d_metadata,
                   &d_subgrids};
-  hipError_t err = hipLaunchKernel(k.func, dim3(p.nr_subgrids),
-                                   dim3(k.block), args, 0, stream);
-  if (err == hipSuccess && k.fallback != nullptr)
-    err = hipLaunchKernel(k.fallback, dim3(p.nr_subgrids), dim3(k.block),
-                          args, 0, stream);
-  return err;
+  return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args, 0,
+                         stream);
 }
 
 namespace {

@@ -106,11 +106,6 @@ struct Extents {
 
 struct KernelChoice {
   const void *func = nullptr;  // __global__ with the 13-argument ABI
-  // Launched after func on the same stream when set: the kernel covering
-  // the subgrids func leaves alone (the MFMA kernels take only mirror-
-  // eligible subgrids; the fallback takes the rest and returns at once on
-  // the others).  Same ABI and launch shape.
-  const void *fallback = nullptr;
   const char *name = "";
   int block = 256;
   int grid = 0;  // = nr_subgrids
