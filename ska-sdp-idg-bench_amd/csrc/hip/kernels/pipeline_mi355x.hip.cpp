@@ -299,12 +299,121 @@ __global__ void __launch_bounds__(256)
     plane[i] = make_float2(src[i].x * scale, src[i].y * scale);
 }
 
+// S = 32 or 64: each thread owns one whole row, then one whole column, of a
+// plane and transforms it in registers (radix-2 decimation in frequency,
+// fully unrolled, so the bit-reversed output order is a compile-time register
+// renaming); the planes pass through LDS once for the transpose (rows padded
+// to N + 1 complex: conflict-free column reads).  A workgroup of 128 threads
+// takes 128 / N planes, loaded and stored coalesced.  Same transform as
+// kernel_subgrid_dft.
+template <int N>
+__device__ __forceinline__ void fft_dif_registers(float2 (&x)[N],
+                                                  const float2 (&tw)[N / 2]) {
+#pragma unroll
+  for (int len = N; len >= 2; len >>= 1) {
+    const int half = len >> 1;
+    const int step = N / len;  // twiddle stride
+#pragma unroll
+    for (int start = 0; start < N; start += len) {
+#pragma unroll
+      for (int j = 0; j < half; ++j) {
+        const float2 a = x[start + j], b = x[start + j + half];
+        x[start + j] = make_float2(a.x + b.x, a.y + b.y);
+        const float2 d = make_float2(a.x - b.x, a.y - b.y);
+        x[start + j + half] = j == 0 ? d : cmulf(d, tw[j * step]);
+      }
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ constexpr int bit_reverse(int i) {
+  int r = 0;
+  for (int b = 1; b < N; b <<= 1) r = (r << 1) | ((i & b) ? 1 : 0);
+  return r;
+}
+
+template <int N>
+__global__ void __launch_bounds__(128)
+    kernel_subgrid_fft_reg(float2 *__restrict__ planes, int nr_planes,
+                           float sign, float scale) {
+  constexpr int P = 128 / N;          // planes per workgroup
+  constexpr int RS = N + 1;           // padded LDS row stride (complex)
+  __shared__ float2 lds[P * N * RS];
+  const int tid = threadIdx.x;
+  const int p0 = blockIdx.x * P;
+  const int np = min(P, nr_planes - p0);
+  float2 *base = planes + static_cast<size_t>(p0) * N * N;
+
+  // coalesced load of the workgroup's planes (contiguous), all loads of a
+  // thread in flight before the first LDS write
+  if (np == P) {
+    constexpr int K = P * N * N / 2 / 128;  // float4 (2 complex) per thread
+    const float4 *b4 = reinterpret_cast<const float4 *>(base);
+    float4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = b4[tid + 128 * k];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = 2 * (tid + 128 * k);  // complex index, even
+      const int pp = i / (N * N), r = i - pp * N * N;
+      float2 *d = lds + pp * N * RS + (r / N) * RS + (r % N);
+      d[0] = make_float2(v[k].x, v[k].y);
+      d[1] = make_float2(v[k].z, v[k].w);
+    }
+  } else {
+    for (int i = tid; i < np * N * N; i += 128) {
+      const int pp = i / (N * N), r = i - pp * N * N;
+      lds[pp * N * RS + (r / N) * RS + (r % N)] = base[i];
+    }
+  }
+  float2 tw[N / 2];
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) tw[k] = unit_phasor(k, N, sign);
+  __syncthreads();
+
+  const int p = tid / N, q = tid % N;  // plane, row (then column)
+  float2 x[N];
+  // rows
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = lds[p * N * RS + q * RS + i];
+  fft_dif_registers<N>(x, tw);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    lds[p * N * RS + q * RS + bit_reverse<N>(i)] = x[i];
+  __syncthreads();
+  // columns
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = lds[p * N * RS + i * RS + q];
+  fft_dif_registers<N>(x, tw);
+  if (p < np) {
+    float2 *out = base + static_cast<size_t>(p) * N * N;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      out[bit_reverse<N>(i) * N + q] =
+          make_float2(x[i].x * scale, x[i].y * scale);
+  }
+}
+
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
                               float scale, void *d_subgrids,
                               hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
   const int S = subgrid_size;
   const float sgn = sign >= 0 ? 1.0f : -1.0f;
+  const int nplanes = 4 * nr_subgrids;
+  if (S == 32) {
+    hipLaunchKernelGGL(kernel_subgrid_fft_reg<32>, dim3((nplanes + 3) / 4),
+                       dim3(128), 0, stream, static_cast<float2 *>(d_subgrids),
+                       nplanes, sgn, scale);
+    return hipGetLastError();
+  }
+  if (S == 64) {
+    hipLaunchKernelGGL(kernel_subgrid_fft_reg<64>, dim3((nplanes + 1) / 2),
+                       dim3(128), 0, stream, static_cast<float2 *>(d_subgrids),
+                       nplanes, sgn, scale);
+    return hipGetLastError();
+  }
   if ((S & (S - 1)) == 0 && S >= 2) {
     int log2S = 0;
     while ((1 << log2S) < S) ++log2S;
