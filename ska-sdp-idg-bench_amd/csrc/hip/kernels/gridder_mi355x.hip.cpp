@@ -336,23 +336,29 @@ __device__ __forceinline__ void grid_mfma(
         }
         __syncthreads();
         // ---- MFMA over the buffered K-steps ----
-        for (int qq = 0; qq < nq; ++qq) {
-          const int t = min((q0 + qq) * 4 + grp, nt - 1);
-          const idg::UVWCoordinate<float> c = uvw[g.time_offset + t];
-          floatx2 np2[PT];
+        // Channel blocks outermost: the block's CB wavenumbers are loaded
+        // into SGPRs once per fill, not once per timestep quad.
+        for (int jb = 0; jb < nj; jb += CB / 4) {
+          const int je = min(jb + CB / 4, nj);
+          const float ka = wavenumbers[4 * (j0 + jb)];
+          float kb[CB];
 #pragma unroll
-          for (int i = 0; i < PT; ++i) {
-            // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
-            // subgrids, where fma(0, n, x) == x
-            const float pidx =
-                MIRROR ? fma_(c.u, lg[i], c.v * mg[i])
-                       : fma_(c.w, ng[i], fma_(c.u, lg[i], c.v * mg[i]));
-            np2[i] = floatx2{-pidx, -pidx};
-          }
-          for (int jb = 0; jb < nj; jb += CB / 4) {
-            const int je = min(jb + CB / 4, nj);
+          for (int v = 0; v < CB; ++v)
+            kb[v] = wavenumbers[min(4 * (j0 + jb) + v, C - 1)];
+          for (int qq = 0; qq < nq; ++qq) {
+            const int t = min((q0 + qq) * 4 + grp, nt - 1);
+            const idg::UVWCoordinate<float> c = uvw[g.time_offset + t];
+            floatx2 np2[PT];
+#pragma unroll
+            for (int i = 0; i < PT; ++i) {
+              // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
+              // subgrids, where fma(0, n, x) == x
+              const float pidx =
+                  MIRROR ? fma_(c.u, lg[i], c.v * mg[i])
+                         : fma_(c.w, ng[i], fma_(c.u, lg[i], c.v * mg[i]));
+              np2[i] = floatx2{-pidx, -pidx};
+            }
             // anchor: phase at the block's first channel
-            const float ka = wavenumbers[4 * (j0 + jb)];
             floatx2 A2[PT], R2[PT];
             static_assert(PT % 2 == 0, "anchors are formed for tile pairs");
 #pragma unroll
@@ -373,11 +379,6 @@ __device__ __forceinline__ void grid_mfma(
               R2[i] = floatx2{r.x, r.x};
               R2[i + 1] = floatx2{r.y, r.y};
             }
-            // the block's CB wavenumbers, wave-uniform (SGPRs)
-            float kb[CB];
-#pragma unroll
-            for (int v = 0; v < CB; ++v)
-              kb[v] = wavenumbers[min(4 * (j0 + jb) + v, C - 1)];
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
               const int jj = jb + u;
