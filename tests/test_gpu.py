@@ -307,20 +307,41 @@ def test_full_size_wterm_sampled_subgrids_vs_oracle(idg, oracle_lib, full_w):
     _sampled_vs_oracle(idg, oracle_lib, *full_w)
 
 
-def _sampled_vs_oracle(idg, oracle_lib, p, a, dev):
+def _rel_rms(a, b):
+    """Scale-free normalised RMS error sqrt(sum|a-b|^2 / sum|b|^2)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(((a - b) ** 2).sum() / max((b ** 2).sum(), 1e-300)))
+
+
+def _sampled_vs_oracle(idg, oracle_lib, p, a, dev, samples=None,
+                       gridder_metric="reference"):
+    """gridder_metric "relative": the reference metric (test_util.hpp:28-92,
+    sum diff^2 / max|x|) is not scale-free and grows with sqrt of the pixel
+    magnitude; at T x C = 32,768 visibilities per pixel even the reference's
+    own CPU output misses 1e-5 against the same sum accumulated in fp64
+    (1.5e-5, tests/debug/grid_fp64.py), so large-K configs are held to the
+    same 1e-5 bar in the scale-free normalised RMS instead."""
     import torch
-    g = _dgrid(idg, p, dev, dev["visibilities"]).cpu().numpy()
-    d = _ddegrid(idg, p, dev, dev["subgrids"]).cpu().numpy()
+    ns = p["nr_subgrids"]
+    samples = samples or (0, 1, 12_345 % ns, ns - 1)
+    g_dev = _dgrid(idg, p, dev, dev["visibilities"])
+    d_dev = _ddegrid(idg, p, dev, dev["subgrids"])
     torch.cuda.synchronize()
     T = a["uvw"].shape[1]
-    for s in (0, 1, 12_345, p["nr_subgrids"] - 1):
+    for s in samples:
+        g = g_dev[s:s + 1].cpu().numpy()
+        d = d_dev[s:s + 1].cpu().numpy()   # uvw rows = subgrids: row s
         md = a["metadata"][s:s + 1]
-        go = np.zeros_like(g[s:s + 1])
+        go = np.zeros_like(g)
         q = dict(p, nr_subgrids=1)
         oracle_lib.gridder(*_params(q), a["uvw"], a["wavenumbers"],
                            a["visibilities"], a["spheroidal"], a["aterms"],
                            md, go)
-        assert oracle_lib.check_error(g[s:s + 1], go)[0] <= TOLERANCE, s
+        if gridder_metric == "relative":
+            assert _rel_rms(g, go) <= TOLERANCE, s
+        else:
+            assert oracle_lib.check_error(g, go)[0] <= TOLERANCE, s
         do = np.zeros_like(a["visibilities"][s:s + 1])
         # the oracle indexes rows from md[0]; pass this subgrid's rows only
         md0 = md.copy()
@@ -329,8 +350,34 @@ def _sampled_vs_oracle(idg, oracle_lib, p, a, dev):
                              a["wavenumbers"], do, a["spheroidal"],
                              a["aterms"], md0,
                              np.ascontiguousarray(a["subgrids"][s:s + 1]))
-        assert oracle_lib.check_error(d[s:s + 1], do)[0] <= TOLERANCE, s
+        assert oracle_lib.check_error(d, do)[0] <= TOLERANCE, s
         assert int(md["nr_timesteps"][0]) == T
+
+
+@pytest.mark.parametrize("cfg", [
+    # BASELINE configs[2] (C = 256) with NR_TIMESLOTS = 4 to bound the
+    # run time: 4,900 subgrids, 5.1 GB of visibilities
+    (50, 4, 128, 256, 1024, 32),
+    # BASELINE configs[4]: S = 64, A-terms + spheroidal, 24,500 subgrids
+    (50, 20, 128, 16, 1024, 64),
+])
+def test_large_configs_sampled_subgrids_vs_oracle(idg, oracle_lib, cfg):
+    import torch
+    st, ts, T, C, G, S = cfg
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    dev = _to_device(a)
+    try:
+        _sampled_vs_oracle(idg, oracle_lib, p, a, dev,
+                           samples=(0, p["nr_subgrids"] // 2,
+                                    p["nr_subgrids"] - 1),
+                           gridder_metric="relative" if T * C > 4096
+                           else "reference")
+    finally:
+        del dev
+        torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("op", ["gridder", "degridder"])
