@@ -112,23 +112,85 @@ __global__ void __launch_bounds__(256)
 // ys = (y + S/2) % S, xs = (x + S/2) % S.
 //
 // A gather, not a scatter: one workgroup owns one 32 x 32 tile of one
-// w-layer, finds the subgrids that overlap it (an ordered scan of the
-// metadata: ballot + prefix per 256-subgrid chunk into an LDS list), adds
-// their pixels into registers in subgrid order and read-modify-writes the
-// tile once.  Every subgrid pixel is read exactly once over the whole
-// launch, there are no atomics, and the summation order -- hence every bit
-// of the grid -- is deterministic.
+// w-layer, adds the pixels of the subgrids overlapping it into registers in
+// ascending subgrid order and read-modify-writes the tile once.  Every
+// subgrid pixel is read exactly once over the whole launch, there are no
+// atomics on the grid, and the summation order -- hence every bit of the
+// grid -- is deterministic.  The overlapping subgrids come from per-tile
+// bins (count -> scan -> fill, then sorted in LDS); a bin larger than the
+// LDS list falls back to an ordered scan of all the metadata, which yields
+// the same order.
 constexpr int kAddTile = 32;      // grid tile edge (pixels)
 constexpr int kAddPix = 4;        // tile pixels per thread (1024 / 256)
 constexpr int kAddMaxTable = 256; // shift phasors kept in LDS for S <= 128
+constexpr int kAddBinCap = 2048;  // bin entries sorted in LDS
 static_assert(kAddTile * kAddTile == 256 * kAddPix, "tile = block x pixels");
+
+struct TileSpan {
+  int tx0, tx1, ty0, ty1;  // inclusive tile ranges a subgrid overlaps
+};
+
+__device__ __forceinline__ TileSpan tile_span(const idg::Metadata &m, int S) {
+  return {m.coordinate.x / kAddTile, (m.coordinate.x + S - 1) / kAddTile,
+          m.coordinate.y / kAddTile, (m.coordinate.y + S - 1) / kAddTile};
+}
+
+// Bins: count (pass 0) or fill (pass 1) the tiles each subgrid overlaps.
+__global__ void __launch_bounds__(256)
+    kernel_adder_bin(const idg::Metadata *__restrict__ metadata,
+                     int nr_subgrids, int G, int S, int nr_w_layers, int pass,
+                     int *__restrict__ count, int *__restrict__ cursor,
+                     int *__restrict__ list) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= nr_subgrids) return;
+  const idg::Metadata m = metadata[s];
+  if (!fits(m, G, S, nr_w_layers)) return;
+  const int ntx = (G + kAddTile - 1) / kAddTile;
+  const TileSpan t = tile_span(m, S);
+  for (int ty = t.ty0; ty <= t.ty1; ++ty)
+    for (int tx = t.tx0; tx <= t.tx1; ++tx) {
+      const int tile = (m.coordinate.z * ntx + ty) * ntx + tx;
+      if (pass == 0)
+        atomicAdd(count + tile, 1);
+      else
+        list[atomicAdd(cursor + tile, 1)] = s;
+    }
+}
+
+// Exclusive scan of the bin counts (one workgroup): offset = cursor.
+__global__ void __launch_bounds__(1024)
+    kernel_adder_bin_scan(const int *__restrict__ count, int n,
+                          int *__restrict__ offset, int *__restrict__ cursor) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  int running = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int v = base + tid < n ? count[base + tid] : 0;
+    part[tid] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+      const int add = tid >= d ? part[tid - d] : 0;
+      __syncthreads();
+      part[tid] += add;
+      __syncthreads();
+    }
+    if (base + tid < n) {
+      offset[base + tid] = running + part[tid] - v;
+      cursor[base + tid] = running + part[tid] - v;
+    }
+    running += part[1023];
+    __syncthreads();
+  }
+}
 
 __global__ void __launch_bounds__(256)
     kernel_adder(const idg::Metadata *__restrict__ metadata, int nr_subgrids,
+                 const int *__restrict__ count, const int *__restrict__ offset,
+                 const int *__restrict__ list,
                  const float2 *__restrict__ subgrids,
                  float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
-  __shared__ int list[256];
-  __shared__ int2 corner[256];
+  __shared__ int keys[kAddBinCap];
+  __shared__ int2 corner[kAddBinCap];
   __shared__ int wave_count[4];
   __shared__ float2 table[kAddMaxTable];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,6 +198,7 @@ __global__ void __launch_bounds__(256)
   const int tx0 = (blockIdx.x % ntx) * kAddTile;
   const int ty0 = (blockIdx.x / ntx) * kAddTile;
   const int z = blockIdx.y;
+  const int tile = z * ntx * ntx + blockIdx.x;
   const int npix = S * S;
   const bool tabled = 2 * S - 1 <= kAddMaxTable;
   // shift phasor depends on x + y only
@@ -149,54 +212,110 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol) acc[j][pol] = make_float2(0.0f, 0.0f);
 
-  for (int base = 0; base < nr_subgrids; base += 256) {
-    const int s = base + tid;
-    bool hit = false;
-    int cx = 0, cy = 0;
-    if (s < nr_subgrids) {
-      const idg::Metadata m = metadata[s];
-      cx = m.coordinate.x;
-      cy = m.coordinate.y;
-      hit = fits(m, G, S, nr_w_layers) && m.coordinate.z == z &&
-            cx < tx0 + kAddTile && cx + S > tx0 && cy < ty0 + kAddTile &&
-            cy + S > ty0;
-    }
-    const unsigned long long mask = __ballot(hit);
-    __syncthreads();  // the previous chunk's list is consumed
-    if (lane == 0) wave_count[wave] = __popcll(mask);
-    __syncthreads();
-    int offset = 0, total = 0;
+  // add the entries [0, total) of the LDS list, in list order; U entries
+  // per step with every load issued before the first add (lanes outside an
+  // entry's subgrid load its pixel 0 and drop it)
+  constexpr int U = 2;
+  auto add_list = [&](int total) {
+    for (int e = 0; e < total; e += U) {
+      float2 v[U][kAddPix][4];
+      float2 ph[U][kAddPix];
+      bool ok[U][kAddPix];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      offset += w < wave ? wave_count[w] : 0;
-      total += wave_count[w];
-    }
-    if (hit) {
-      const int pos =
-          offset + __popcll(mask & ((1ull << lane) - 1ull));  // ordered
-      list[pos] = s;
-      corner[pos] = make_int2(cx, cy);
-    }
-    __syncthreads();
-    for (int e = 0; e < total; ++e) {
-      const int2 c = corner[e];
-      const float2 *sg = subgrids + static_cast<size_t>(list[e]) * 4 * npix;
+      for (int h = 0; h < U; ++h) {
+        const int ee = min(e + h, total - 1);
+        const int2 c = corner[ee];
+        const float2 *sg =
+            subgrids + static_cast<size_t>(keys[ee]) * 4 * npix;
 #pragma unroll
-      for (int j = 0; j < kAddPix; ++j) {
-        const int i = tid + 256 * j;
-        const int x = tx0 + (i & (kAddTile - 1)) - c.x;
-        const int y = ty0 + i / kAddTile - c.y;
-        if (x < 0 || x >= S || y < 0 || y >= S) continue;
-        const int src = ((y + S / 2) % S) * S + (x + S / 2) % S;
-        const float2 ph =
-            tabled ? table[x + y] : shift_phasor(x, y, S, 1.0f);
+        for (int j = 0; j < kAddPix; ++j) {
+          const int i = tid + 256 * j;
+          const int x = tx0 + (i & (kAddTile - 1)) - c.x;
+          const int y = ty0 + i / kAddTile - c.y;
+          ok[h][j] = e + h < total && x >= 0 && x < S && y >= 0 && y < S;
+          const int src =
+              ok[h][j] ? ((y + S / 2) % S) * S + (x + S / 2) % S : 0;
+          ph[h][j] = !ok[h][j] ? make_float2(0.0f, 0.0f)
+                     : tabled  ? table[x + y]
+                               : shift_phasor(x, y, S, 1.0f);
 #pragma unroll
-        for (int pol = 0; pol < 4; ++pol) {
-          const float2 v = cmulf(ph, sg[pol * npix + src]);
-          acc[j][pol].x += v.x;
-          acc[j][pol].y += v.y;
+          for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = sg[pol * npix + src];
         }
       }
+#pragma unroll
+      for (int h = 0; h < U; ++h)
+#pragma unroll
+        for (int j = 0; j < kAddPix; ++j) {
+          if (!ok[h][j]) continue;
+#pragma unroll
+          for (int pol = 0; pol < 4; ++pol) {
+            const float2 w = cmulf(ph[h][j], v[h][j][pol]);
+            acc[j][pol].x += w.x;
+            acc[j][pol].y += w.y;
+          }
+        }
+    }
+  };
+
+  const int n = count[tile];
+  if (n <= kAddBinCap) {
+    // the bin, sorted ascending (bitonic over the next power of two)
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    const int off = offset[tile];
+    for (int i = tid; i < n2; i += 256) keys[i] = i < n ? list[off + i] : 0x7fffffff;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < n2; i += 256) {
+          const int l = i ^ j;
+          if (l > i) {
+            const int a = keys[i], b = keys[l];
+            if (((i & k) == 0) == (a > b)) {
+              keys[i] = b;
+              keys[l] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int e = tid; e < n; e += 256) {
+      const idg::Metadata m = metadata[keys[e]];
+      corner[e] = make_int2(m.coordinate.x, m.coordinate.y);
+    }
+    __syncthreads();
+    add_list(n);
+  } else {
+    // ordered scan of all the metadata, 256 subgrids at a time
+    for (int base = 0; base < nr_subgrids; base += 256) {
+      const int s = base + tid;
+      bool hit = false;
+      int cx = 0, cy = 0;
+      if (s < nr_subgrids) {
+        const idg::Metadata m = metadata[s];
+        cx = m.coordinate.x;
+        cy = m.coordinate.y;
+        hit = fits(m, G, S, nr_w_layers) && m.coordinate.z == z &&
+              cx < tx0 + kAddTile && cx + S > tx0 && cy < ty0 + kAddTile &&
+              cy + S > ty0;
+      }
+      const unsigned long long mask = __ballot(hit);
+      __syncthreads();  // the previous chunk's list is consumed
+      if (lane == 0) wave_count[wave] = __popcll(mask);
+      __syncthreads();
+      int pos = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        pos += w < wave ? wave_count[w] : 0;
+        total += wave_count[w];
+      }
+      if (hit) {
+        pos += __popcll(mask & ((1ull << lane) - 1ull));  // ordered
+        keys[pos] = s;
+        corner[pos] = make_int2(cx, cy);
+      }
+      __syncthreads();
+      add_list(total);
     }
   }
 
@@ -439,13 +558,39 @@ hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
                         hipStream_t stream) {
   if (nr_subgrids <= 0 || nr_w_layers <= 0 || grid_size <= 0)
     return hipSuccess;
+  const int S = subgrid_size;
   const int ntx = (grid_size + kAddTile - 1) / kAddTile;
-  hipLaunchKernelGGL(kernel_adder, dim3(ntx * ntx, nr_w_layers), dim3(256), 0,
-                     stream, static_cast<const idg::Metadata *>(d_metadata),
-                     nr_subgrids, static_cast<const float2 *>(d_subgrids),
-                     static_cast<float2 *>(d_grid), grid_size, subgrid_size,
-                     nr_w_layers);
-  return hipGetLastError();
+  const size_t ntiles = static_cast<size_t>(nr_w_layers) * ntx * ntx;
+  const int span = (S + kAddTile - 2) / kAddTile + 1;  // tiles per axis, max
+  const size_t nlist = static_cast<size_t>(nr_subgrids) * span * span;
+  // stream-ordered workspace: count | offset | cursor | list
+  int *ws = nullptr;
+  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&ws),
+                                  (3 * ntiles + nlist) * sizeof(int), stream);
+  if (err != hipSuccess) return err;
+  int *count = ws, *offset = ws + ntiles, *cursor = ws + 2 * ntiles;
+  int *list = ws + 3 * ntiles;
+  const auto *md = static_cast<const idg::Metadata *>(d_metadata);
+  const int nb = (nr_subgrids + 255) / 256;
+  err = hipMemsetAsync(count, 0, ntiles * sizeof(int), stream);
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL(kernel_adder_bin, dim3(nb), dim3(256), 0, stream, md,
+                       nr_subgrids, grid_size, S, nr_w_layers, 0, count,
+                       cursor, list);
+    hipLaunchKernelGGL(kernel_adder_bin_scan, dim3(1), dim3(1024), 0, stream,
+                       count, static_cast<int>(ntiles), offset, cursor);
+    hipLaunchKernelGGL(kernel_adder_bin, dim3(nb), dim3(256), 0, stream, md,
+                       nr_subgrids, grid_size, S, nr_w_layers, 1, count,
+                       cursor, list);
+    hipLaunchKernelGGL(kernel_adder, dim3(ntx * ntx, nr_w_layers), dim3(256),
+                       0, stream, md, nr_subgrids, count, offset, list,
+                       static_cast<const float2 *>(d_subgrids),
+                       static_cast<float2 *>(d_grid), grid_size, S,
+                       nr_w_layers);
+    err = hipGetLastError();
+  }
+  const hipError_t ferr = hipFreeAsync(ws, stream);
+  return err != hipSuccess ? err : ferr;
 }
 
 hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
