@@ -203,7 +203,10 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 // (x, x, y, y) per lane, stored pre-expanded in LDS.  Per phasor: 1.5 packed
 // phase instructions, v_sin + v_cos, 3 split instructions, half an MFMA.
 // ---------------------------------------------------------------------------
-constexpr int kKsBuf = 16;  // K-steps (16 items each) of B fragments per fill
+#ifndef IDG_GRID_KSBUF
+#define IDG_GRID_KSBUF 32
+#endif
+constexpr int kKsBuf = IDG_GRID_KSBUF;  // K-steps (16 items each) of B fragments per fill
 
 // NW waves per workgroup, PT 16-pixel tiles per wave: NW * 16 * PT base
 // pixels per pass, and each B fragment is built once per pass.
@@ -211,8 +214,10 @@ template <int PT, int NW>
 struct MfmaLds {
   static constexpr int kObufFloats = 2 * NW * 16 * PT * 16;  // X and Y tiles
   static constexpr int kBbufWords = kKsBuf * 64 * 8;  // uint4 X + uint4 Y
-  static constexpr int kWords =
-      (kObufFloats > kBbufWords ? kObufFloats : kBbufWords) + 8;
+  // uvw of the fill's timesteps (at most 4 * kKsBuf), float4 each
+  static constexpr int kUvwOff =
+      kObufFloats > kBbufWords ? kObufFloats : kBbufWords;
+  static constexpr int kWords = kUvwOff + 4 * 4 * kKsBuf + 8;
 };
 
 template <int S_CT, int PT, int CB, int NW, bool MIRROR>
@@ -260,20 +265,28 @@ __device__ __forceinline__ void grid_mfma(
 
   uint4 *bbuf = reinterpret_cast<uint4 *>(lds);  // [ks][64][X, Y]
   float *obuf = reinterpret_cast<float *>(lds);
+  float4 *tuvw = reinterpret_cast<float4 *>(lds + MfmaLds<PT, NW>::kUvwOff);
   const int nquads = (nt + 3) / 4;
   const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
   const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
 
   constexpr int kPass = NW * 16 * PT;  // base pixels per pass
   for (int gbase = 0; gbase < half; gbase += kPass) {
-    float lg[PT], mg[PT], ng[PT];
-    floatx2 pg2[PT];
+    // Pixel terms of tile pairs (2h, 2h+1), packed: every phase operation
+    // below is one v_pk_* over the pair with the channel's wavenumber
+    // broadcast from an SGPR, so no operand has to be duplicated.
+    static_assert(PT % 2 == 0, "phases are packed over tile pairs");
+    constexpr int PH = PT / 2;
+    floatx2 L2[PH], M2[PH], N2[PH], PG2[PH];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
-      float pg;
-      pixel_geometry(b, S, image_size, g, lg[i], mg[i], ng[i], pg);
-      pg2[i] = floatx2{pg, pg};
+      float l, m, n, pg;
+      pixel_geometry(b, S, image_size, g, l, m, n, pg);
+      L2[i / 2][i % 2] = l;
+      M2[i / 2][i % 2] = m;
+      N2[i / 2][i % 2] = n;
+      PG2[i / 2][i % 2] = pg;
     }
     floatx4 accx[PT], accy[PT];
 #pragma unroll
@@ -333,6 +346,12 @@ __device__ __forceinline__ void grid_mfma(
             bbuf[(ks * 64 + lane) * 2] = make_uint4(xc, xc, yc, yc);
             bbuf[(ks * 64 + lane) * 2 + 1] = make_uint4(xs, xs, ys, ys);
           }
+          // the fill's timesteps' uvw, so the MFMA loop reads LDS, not HBM
+          for (int i = tid; i < nq * 4; i += NW * 64) {
+            const idg::UVWCoordinate<float> c =
+                uvw[g.time_offset + min(q0 * 4 + i, nt - 1)];
+            tuvw[i] = make_float4(c.u, c.v, c.w, 0.0f);
+          }
         }
         __syncthreads();
         // ---- MFMA over the buffered K-steps ----
@@ -346,68 +365,66 @@ __device__ __forceinline__ void grid_mfma(
           for (int v = 0; v < CB; ++v)
             kb[v] = wavenumbers[min(4 * (j0 + jb) + v, C - 1)];
           for (int qq = 0; qq < nq; ++qq) {
-            const int t = min((q0 + qq) * 4 + grp, nt - 1);
-            const idg::UVWCoordinate<float> c = uvw[g.time_offset + t];
-            floatx2 np2[PT];
+            const float4 c4 = tuvw[qq * 4 + grp];
+            const idg::UVWCoordinate<float> c = {c4.x, c4.y, c4.z};
+            const floatx2 cu = {c.u, c.u}, cv = {c.v, c.v};
+            const floatx2 ih = {kInv2PiHi, kInv2PiHi};
+            floatx2 NP[PH], A2[PH], R2[PH];
 #pragma unroll
-            for (int i = 0; i < PT; ++i) {
+            for (int h = 0; h < PH; ++h) {
               // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
               // subgrids, where fma(0, n, x) == x
-              const float pidx =
-                  MIRROR ? fma_(c.u, lg[i], c.v * mg[i])
-                         : fma_(c.w, ng[i], fma_(c.u, lg[i], c.v * mg[i]));
-              np2[i] = floatx2{-pidx, -pidx};
-            }
-            // anchor: phase at the block's first channel
-            floatx2 A2[PT], R2[PT];
-            static_assert(PT % 2 == 0, "anchors are formed for tile pairs");
-#pragma unroll
-            for (int i = 0; i < PT; i += 2) {
-              // revolutions() of two tiles' anchors in packed arithmetic
-              const floatx2 a = __builtin_elementwise_fma(
-                  floatx2{np2[i].x, np2[i + 1].x}, floatx2{ka, ka},
-                  floatx2{pg2[i].x, pg2[i + 1].x});
-              const floatx2 ih = {kInv2PiHi, kInv2PiHi};
+              floatx2 pidx = __builtin_elementwise_fma(cu, L2[h], cv * M2[h]);
+              if constexpr (!MIRROR)
+                pidx = __builtin_elementwise_fma(floatx2{c.w, c.w}, N2[h],
+                                                 pidx);
+              NP[h] = -pidx;
+              // anchor: phase at the block's first channel, in revolutions
+              const floatx2 a =
+                  __builtin_elementwise_fma(NP[h], floatx2{ka, ka}, PG2[h]);
               const floatx2 hi = a * ih;
               floatx2 lo = __builtin_elementwise_fma(a, ih, -hi);
               lo = __builtin_elementwise_fma(
                   a, floatx2{kInv2PiLo, kInv2PiLo}, lo);
               const floatx2 rn = {__builtin_rintf(hi.x), __builtin_rintf(hi.y)};
-              const floatx2 r = (hi - rn) + lo;
-              A2[i] = floatx2{a.x, a.x};
-              A2[i + 1] = floatx2{a.y, a.y};
-              R2[i] = floatx2{r.x, r.x};
-              R2[i + 1] = floatx2{r.y, r.y};
+              A2[h] = a;
+              R2[h] = (hi - rn) + lo;
             }
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
               const int jj = jb + u;
               if (jj >= je) break;
-              const floatx2 k01 = {kb[4 * u], kb[4 * u + 1]};
-              const floatx2 k23 = {kb[4 * u + 2], kb[4 * u + 3]};
               const int ks = qq * nj + jj;
               const uint4 bx = bbuf[(ks * 64 + lane) * 2];
               const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
               const half8 bfx = pack4(bx.x, bx.y, bx.z, bx.w);
               const half8 bfy = pack4(by.x, by.y, by.z, by.w);
-              const floatx2 inv2pi = {kInv2PiHi, kInv2PiHi};
 #pragma unroll
-              for (int i = 0; i < PT; ++i) {
-                const floatx2 p01 = __builtin_elementwise_fma(np2[i], k01,
-                                                              pg2[i]);
-                const floatx2 p23 = __builtin_elementwise_fma(np2[i], k23,
-                                                              pg2[i]);
-                const floatx2 r01 =
-                    __builtin_elementwise_fma(p01 - A2[i], inv2pi, R2[i]);
-                const floatx2 r23 =
-                    __builtin_elementwise_fma(p23 - A2[i], inv2pi, R2[i]);
-                float s0, c0f, s1, c1f, s2, c2f, s3, c3f;
-                sincos_rev(r01.x, &s0, &c0f);
-                sincos_rev(r01.y, &s1, &c1f);
-                sincos_rev(r23.x, &s2, &c2f);
-                sincos_rev(r23.y, &s3, &c3f);
-                accx[i] = mfma16(split_quad(c0f, c1f, c2f, c3f), bfx, accx[i]);
-                accy[i] = mfma16(split_quad(s0, s1, s2, s3), bfy, accy[i]);
+              for (int h = 0; h < PH; ++h) {
+                // r[j] = (revolutions of channel 4u+j) for tiles (2h, 2h+1)
+                float snx[4], csx[4], sny[4], csy[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const float kj = kb[4 * u + j];
+                  const floatx2 ph =
+                      __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
+                  const floatx2 r =
+                      __builtin_elementwise_fma(ph - A2[h], ih, R2[h]);
+                  sincos_rev(r.x, &snx[j], &csx[j]);
+                  sincos_rev(r.y, &sny[j], &csy[j]);
+                }
+                accx[2 * h] = mfma16(
+                    split_quad(csx[0], csx[1], csx[2], csx[3]), bfx,
+                    accx[2 * h]);
+                accy[2 * h] = mfma16(
+                    split_quad(snx[0], snx[1], snx[2], snx[3]), bfy,
+                    accy[2 * h]);
+                accx[2 * h + 1] = mfma16(
+                    split_quad(csy[0], csy[1], csy[2], csy[3]), bfx,
+                    accx[2 * h + 1]);
+                accy[2 * h + 1] = mfma16(
+                    split_quad(sny[0], sny[1], sny[2], sny[3]), bfy,
+                    accy[2 * h + 1]);
               }
               // Keep each K-step's MFMAs inside its own iteration.  When the
               // scheduler sank all of an iteration's MFMAs to the end of the
