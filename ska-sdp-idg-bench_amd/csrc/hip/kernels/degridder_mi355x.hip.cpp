@@ -301,8 +301,10 @@ __device__ __forceinline__ void degrid_mfma(
               sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1
               sincos_rev(rx.y, &s2, &c2);  // channel j+1, pixel 0
               sincos_rev(ry.y, &s3, &c3);  // channel j+1, pixel 1
-              acc[j] = mfma16(split_quad(c0, c1, s0, s1), bf, acc[j]);
-              acc[j + 1] = mfma16(split_quad(c2, c3, s2, s3), bf, acc[j + 1]);
+              half8 a01, a23;  // one asm block (one pair of pads) for both
+              split_oct(c0, c1, s0, s1, c2, c3, s2, s3, &a01, &a23);
+              acc[j] = mfma16(a01, bf, acc[j]);
+              acc[j + 1] = mfma16(a23, bf, acc[j + 1]);
             }
           }
           // one K-step's MFMAs stay in their iteration

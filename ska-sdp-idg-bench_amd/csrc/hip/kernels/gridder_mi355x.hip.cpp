@@ -413,18 +413,17 @@ __device__ __forceinline__ void grid_mfma(
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
-                accx[2 * h] = mfma16(
-                    split_quad(csx[0], csx[1], csx[2], csx[3]), bfx,
-                    accx[2 * h]);
-                accy[2 * h] = mfma16(
-                    split_quad(snx[0], snx[1], snx[2], snx[3]), bfy,
-                    accy[2 * h]);
-                accx[2 * h + 1] = mfma16(
-                    split_quad(csy[0], csy[1], csy[2], csy[3]), bfx,
-                    accx[2 * h + 1]);
-                accy[2 * h + 1] = mfma16(
-                    split_quad(sny[0], sny[1], sny[2], sny[3]), bfy,
-                    accy[2 * h + 1]);
+                // one asm block splits a tile's cos and sin quads (one pair of
+                // wait-state pads for both MFMA operands)
+                half8 ac, as;
+                split_oct(csx[0], csx[1], csx[2], csx[3], snx[0], snx[1],
+                          snx[2], snx[3], &ac, &as);
+                accx[2 * h] = mfma16(ac, bfx, accx[2 * h]);
+                accy[2 * h] = mfma16(as, bfy, accy[2 * h]);
+                split_oct(csy[0], csy[1], csy[2], csy[3], sny[0], sny[1],
+                          sny[2], sny[3], &ac, &as);
+                accx[2 * h + 1] = mfma16(ac, bfx, accx[2 * h + 1]);
+                accy[2 * h + 1] = mfma16(as, bfy, accy[2 * h + 1]);
               }
               // Keep each K-step's MFMAs inside its own iteration.  When the
               // scheduler sank all of an iteration's MFMAs to the end of the

@@ -114,6 +114,35 @@ __device__ __forceinline__ half8 split_quad(float a0, float a1, float b0,
   return pack4(h0, l0, h1, l1);
 }
 
+// Two split_quad()s in one asm block (one pair of pads for both operands):
+// *A = split of (a0, a1, a2, a3), *B = split of (b0, b1, b2, b3).
+__device__ __forceinline__ void split_oct(float a0, float a1, float a2,
+                                          float a3, float b0, float b1,
+                                          float b2, float b3, half8 *A,
+                                          half8 *B) {
+  unsigned h0, l0, h1, l1, h2, l2, h3, l3;
+  asm("s_nop 0\n\t"
+      "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %2, %10, %11\n\t"
+      "v_cvt_pk_f16_f32 %4, %12, %13\n\t"
+      "v_cvt_pk_f16_f32 %6, %14, %15\n\t"
+      "v_fma_mixlo_f16 %1, %0, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, %2, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %4, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %6, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %0, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, %2, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %4, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %6, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(h0), "=&v"(l0), "=&v"(h1), "=&v"(l1), "=&v"(h2), "=&v"(l2),
+        "=&v"(h3), "=&v"(l3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2),
+        "v"(b3));
+  *A = pack4(h0, l0, h1, l1);
+  *B = pack4(h2, l2, h3, l3);
+}
+
 __device__ __forceinline__ floatx4 mfma16(const half8 &a, const half8 &b,
                                           const floatx4 &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
