@@ -120,6 +120,41 @@ struct DegridMfmaLds {
   static constexpr int kWords = kGeoWords + kBfrWords;
 };
 
+// Revolutions of the phases of one pixel at the channel pair kp = (k_j,
+// k_j+1):  fma(fma(p, k, o) - A, 1/2pi, R)  with p, o, A, R taken from half H
+// of their (pixel 0, pixel 1) VGPR pairs and broadcast to both lanes by
+// op_sel, so no operand is duplicated into a register pair (hipcc otherwise
+// materialises the broadcasts or splits the packed FMA into two).  The
+// constant is the inline 1/(2 pi) = kInv2PiHi.  A dependent packed-f32 VALU
+// pair gets one wait state (s_nop 0), as hipcc pads its own; the output is
+// read by compiler code, which pads after the asm itself.
+template <int H>
+__device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
+                                                   floatx2 o, floatx2 A,
+                                                   floatx2 R) {
+  floatx2 r;
+  if constexpr (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_add_f32 %0, %0, %4 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %5 op_sel_hi:[1,0,0]"
+        : "=&v"(r)
+        : "v"(p), "s"(kp), "v"(o), "v"(A), "v"(R));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,1,1]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_add_f32 %0, %0, %4 op_sel:[0,1] op_sel_hi:[1,1] "
+        "neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %5 op_sel:[0,0,1] "
+        "op_sel_hi:[1,0,1]"
+        : "=&v"(r)
+        : "v"(p), "s"(kp), "v"(o), "v"(A), "v"(R));
+  return r;
+}
+static_assert(kInv2PiHi == 0.15915494f, "phase_rev_bcast's inline constant");
+
 template <int S_CT, int CT, int CB, int KP, bool MIRROR>
 __device__ __forceinline__ void degrid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
@@ -232,7 +267,6 @@ __device__ __forceinline__ void degrid_mfma(
   // chunk never overlaps live accumulators (no spills); each chunk's partial
   // sums are added to the visibilities its own lanes wrote for the previous
   // chunk (same lane, same address: ordered, no atomics).
-  const floatx2 inv2pi = {kInv2PiHi, kInv2PiHi};
   for (int pc0 = 0; pc0 < half; pc0 += KP) {
     if (!single) {
       __syncthreads();
@@ -282,20 +316,15 @@ __device__ __forceinline__ void degrid_mfma(
                 (hi - floatx2{__builtin_rintf(hi.x), __builtin_rintf(hi.y)}) +
                 lo;
             // Packed over channel pairs (j, j+1) per pixel: the wavenumber
-            // pair is one SGPR pair and pixel terms broadcast, so the phase
-            // is one v_pk_fma per two phasors (same fma(pidx, k, -poff)
-            // rounding as the scalar form).
-            const floatx2 Ax = {A.x, A.x}, Ay = {A.y, A.y};
-            const floatx2 Rx = {R.x, R.x}, Ry = {R.y, R.y};
-            const floatx2 px = {pidx.x, pidx.x}, py = {pidx.y, pidx.y};
-            const floatx2 ox = {npoff.x, npoff.x}, oy = {npoff.y, npoff.y};
+            // pair is one SGPR pair and the pixel's terms are broadcast from
+            // their halves of the (pixel 0, pixel 1) pairs by op_sel, so the
+            // phase chain is three v_pk_* per two phasors (same
+            // fma(pidx, k, -poff) rounding as the scalar form).
 #pragma unroll
             for (int j = jb; j < jb + CB; j += 2) {
               const floatx2 kp = {kk[j], kk[j + 1]};
-              const floatx2 rx = __builtin_elementwise_fma(
-                  __builtin_elementwise_fma(px, kp, ox) - Ax, inv2pi, Rx);
-              const floatx2 ry = __builtin_elementwise_fma(
-                  __builtin_elementwise_fma(py, kp, oy) - Ay, inv2pi, Ry);
+              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, A, R);
+              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, A, R);
               float s0, c0, s1, c1, s2, c2, s3, c3;
               sincos_rev(rx.x, &s0, &c0);  // channel j,   pixel 0
               sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1
