@@ -197,6 +197,34 @@ def traffic_for(path, workload, kernel):
         return None
 
 
+def reference_hip_for(workload, sec_per_step, t_grid, t_degrid):
+    """The reference's own HIP kernels measured on MI355X at configs[1]
+    (profiles/reference_hip.json, made by tests/debug/ref_hip.sh): this
+    run's per-GPU rates over theirs, for the fastest reference kernels and
+    for the fastest that pass the reference's own -c check."""
+    if workload != "default":
+        return None
+    try:
+        with open(os.path.join(REPO, "profiles", "reference_hip.json")) as f:
+            ref = json.load(f)
+    except Exception:
+        return None
+    out = {"source": "profiles/reference_hip.json "
+                     "(profiles/r01/reference_hip/SUMMARY.md)"}
+    for tag in ("fastest", "fastest_passing"):
+        r = ref[tag]
+        step = (r["gridder_ms"] + r["degridder_ms"]) / 1e3
+        out[tag] = {
+            "kernels": f"{r['gridder']} ({r['gridder_c']} -c) + "
+                       f"{r['degridder']} ({r['degridder_c']} -c)",
+            "mvis_s_per_gpu": round(ref["mvis_per_step"] / step, 2),
+            "speedup_step": round(step / sec_per_step, 2),
+            "speedup_gridder": round(r["gridder_ms"] / 1e3 / t_grid, 2),
+            "speedup_degridder": round(r["degridder_ms"] / 1e3 / t_degrid, 2),
+        }
+    return out
+
+
 def issue_for(path, workload, kernel):
     """VALU-issue utilisation of a kernel from its committed PMC summary."""
     try:
@@ -446,6 +474,8 @@ def main():
         "roofline_hbm": roofline_hbm,
         "pipeline": pipeline,
         "energy": energy,
+        "reference_hip_mi355x": reference_hip_for(
+            args.workload, sec_per_step, t_grid, t_degrid),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
