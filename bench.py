@@ -153,7 +153,11 @@ def cpu_baseline_threads(w, a, impl, kind, args, nsample, extra):
     T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
     bounds = np.linspace(0, n, cores + 1).astype(int)
     sg = np.zeros((n, 4, S, S, 2), np.float32)
-    vis = np.zeros_like(a["visibilities"][:md_all[n - 1]["time_offset"] + T])
+    # visibilities are [rows / T][T][C][4] complex: the blocks the first n
+    # subgrids' rows (time_offset + t) fall in
+    rows = int(md_all[n - 1]["time_offset"]) + T
+    vis = np.zeros(((rows + T - 1) // T,) + a["visibilities"].shape[1:],
+                   np.float32)
     sub_in = np.ascontiguousarray(a["subgrids"][:n])
 
     def run(fn, i):
@@ -175,6 +179,7 @@ def cpu_baseline_threads(w, a, impl, kind, args, nsample, extra):
         list(pool.map(lambda i: run("d", i), range(cores)))
         t2 = time.perf_counter()
     nvis = n * T * C
+    cpu_baseline_threads.last_outputs = {"subgrids": sg, "visibilities": vis}
     return {
         "value": round(nvis / (t2 - t0) / 1e6, 4),
         "cores": cores,

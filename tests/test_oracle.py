@@ -5,6 +5,8 @@ tests/golden/*.npz were produced by the reference's own CPU path
 the reference's flags; tests/golden/make_golden.py).  The plain-C restatement
 (oracle/idg_oracle.c) must reproduce them far inside the repo tolerance.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -52,6 +54,38 @@ def test_oracle_multithreaded_identical(oracle_lib):
                            a["visibilities"], a["spheroidal"], a["aterms"],
                            a["metadata"], out, nthreads=nt)
     assert np.array_equal(g1, g4)
+
+
+def test_cpu_baseline_threads_compute_the_whole_batch():
+    # bench.py's 16-thread cpu_baseline runs the reference kernel on disjoint
+    # subgrid ranges; with equal baseline offsets (the synthetic batch) the
+    # ranges' outputs are exactly the whole run's
+    import bench
+    import idg_amd
+    os.environ["IDG_CPU_BASELINE_THREADS"] = "3"
+    w = dict(bench.WORKLOADS["default"], nr_stations=4, nr_timeslots=2,
+             nr_timesteps=8, nr_channels=4, grid_size=256, subgrid_size=16)
+    a = idg_amd.generate(4, 2, 8, 4, 256, 16)
+    try:
+        r = bench.cpu_baseline(w, a, 4)
+    finally:
+        del os.environ["IDG_CPU_BASELINE_THREADS"]
+    assert r["cores"] == 3 and r["single_thread"]["cores"] == 1
+    assert r["value"] > 0 and r["unit"] == "Mvis/s"
+    outs = bench.cpu_baseline_threads.last_outputs
+    ns = outs["subgrids"].shape[0]
+    g = np.zeros_like(outs["subgrids"])
+    impl = orc.Reference(portable=True) if orc.Reference.available() \
+        else orc.Oracle()
+    impl.gridder(ns, 256, 16, 0.01, 0.0, 4, 4, a["uvw"], a["wavenumbers"],
+                 a["visibilities"], a["spheroidal"], a["aterms"],
+                 a["metadata"][:ns], g)
+    assert np.array_equal(g, outs["subgrids"])
+    d = np.zeros_like(outs["visibilities"])
+    impl.degridder(ns, 256, 16, 0.01, 0.0, 4, 4, a["uvw"], a["wavenumbers"],
+                   d, a["spheroidal"], a["aterms"], a["metadata"][:ns],
+                   np.ascontiguousarray(a["subgrids"][:ns]))
+    assert np.array_equal(d, outs["visibilities"])
 
 
 def test_metric_matches_numpy_twin(oracle_lib):
