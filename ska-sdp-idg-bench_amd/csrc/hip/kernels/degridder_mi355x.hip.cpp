@@ -174,28 +174,6 @@ __device__ __forceinline__ void degrid_mfma(
   const int half = MIRROR ? npix / 2 : npix;
   const int nt = g.nr_timesteps;
 
-  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range.
-  float vmax = 0.0f;
-  for (int p = tid; p < npix; p += kBlock) {
-    float4 pa, pb, geo;
-    pixel_entry(p, S, npix, image_size, g, nr_stations, spheroidal, aterms,
-                sg, pa, pb, geo);
-    vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(fabsf(pa.x), fabsf(pa.y)),
-                                   fmaxf(fabsf(pa.z), fabsf(pa.w))),
-                             fmaxf(fmaxf(fabsf(pb.x), fabsf(pb.y)),
-                                   fmaxf(fabsf(pb.z), fabsf(pb.w)))));
-  }
-  for (int off = 32; off > 0; off >>= 1)
-    vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-  float *red = reinterpret_cast<float *>(lds);
-  if (lane == 0) red[wave] = vmax;
-  __syncthreads();
-  vmax = 2.0f * fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();  // red[] is geometry space from here on
-  int e = 0;
-  if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
-  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
-
   // pair geometry, structure of arrays: l[KP], m[KP], phase_offset[KP]
   float *geo_l = reinterpret_cast<float *>(lds);
   float *geo_m = geo_l + KP;
@@ -203,65 +181,123 @@ __device__ __forceinline__ void degrid_mfma(
   float *geo_n = geo_o + KP;
   uint2 *bfr = reinterpret_cast<uint2 *>(lds + L::kGeoWords);
   const bool single = half <= KP;
+  // the workgroup max of |P'| lands in red[] (the first geometry words,
+  // before any geometry is written)
+  float *red = reinterpret_cast<float *>(lds);
+  auto block_max = [&](float v) {
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();  // red[] is geometry space from here on
+    return v;
+  };
+  auto absmax = [](const float4 &a, const float4 &b) {
+    return fmaxf(fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)),
+                       fmaxf(fabsf(a.z), fabsf(a.w))),
+                 fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)),
+                       fmaxf(fabsf(b.z), fabsf(b.w))));
+  };
 
+  // Pixel entries P' (and geometry) of pairs pc0 + 2q + h, h = 0, 1, of
+  // K-block q: base in pa/pb, mirror in ma/mb (zero on general subgrids).
+  struct Block {
+    float4 pa[2], pb[2], ma[2], mb[2], geo[2];
+  };
+  auto entries = [&](int pc0, int q, Block &k) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = pc0 + 2 * q + h;
+      const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      k.pa[h] = k.pb[h] = k.ma[h] = k.mb[h] = k.geo[h] = z;
+      if (b < half) {
+        pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
+                    aterms, sg, k.pa[h], k.pb[h], k.geo[h]);
+        if constexpr (MIRROR) {
+          float4 mgeo;
+          pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
+                      spheroidal, aterms, sg, k.ma[h], k.mb[h], mgeo);
+        }
+      }
+    }
+  };
+  // S = P'_b + P'_m and D = P'_b - P'_m of K-block q, scaled, split, and
+  // written as the 16 column lanes' B fragments; the pairs' geometry too.
+  auto store_block = [&](int q, const Block &k, float scale) {
+    float sre[2][4], sim[2][4], dre[2][4], dim[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float pr[4] = {k.pa[h].x, k.pa[h].z, k.pb[h].x, k.pb[h].z};
+      const float pi[4] = {k.pa[h].y, k.pa[h].w, k.pb[h].y, k.pb[h].w};
+      const float mr[4] = {k.ma[h].x, k.ma[h].z, k.mb[h].x, k.mb[h].z};
+      const float mi[4] = {k.ma[h].y, k.ma[h].w, k.mb[h].y, k.mb[h].w};
+#pragma unroll
+      for (int cr = 0; cr < 4; ++cr) {
+        sre[h][cr] = (pr[cr] + mr[cr]) * scale;
+        sim[h][cr] = (pi[cr] + mi[cr]) * scale;
+        dre[h][cr] = (pr[cr] - mr[cr]) * scale;
+        dim[h][cr] = (pi[cr] - mi[cr]) * scale;
+      }
+      geo_l[2 * q + h] = k.geo[h].x;
+      geo_m[2 * q + h] = k.geo[h].y;
+      geo_o[2 * q + h] = k.geo[h].w;
+      if constexpr (!MIRROR) geo_n[2 * q + h] = k.geo[h].z;
+    }
+    // lane (g, col) of K-step ks: ks = q / 4, g = q % 4
+    uint2 *dst = bfr + (q >> 2) * 64 + (q & 3) * 16;
+#pragma unroll
+    for (int cl = 0; cl < 16; ++cl) {
+      const int cr = (cl & 7) >> 1;
+      const bool im = cl & 1;
+      const float bc0 = im ? sim[0][cr] : sre[0][cr];
+      const float bc1 = im ? sim[1][cr] : sre[1][cr];
+      const float bs0 = im ? dre[0][cr] : -dim[0][cr];
+      const float bs1 = im ? dre[1][cr] : -dim[1][cr];
+      dst[cl] = (cl & 8) ? make_uint2(split_lo(bc0, bc1), split_lo(bs0, bs1))
+                         : make_uint2(split_hi(bc0, bc1), split_hi(bs0, bs1));
+    }
+  };
+
+  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range.
+  auto scale_exp = [](float vmax) {
+    int e = 0;
+    if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
+    return e;
+  };
+  int e;
+  static_assert(KP / 2 == kBlock, "one K-block per thread in a single chunk");
+  if (single) {
+    // one chunk: every thread computes its K-block's entries once, the
+    // workgroup max sets the scale, and the same registers are split
+    Block k;
+    entries(0, tid, k);
+    float v = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      v = fmaxf(v, fmaxf(absmax(k.pa[h], k.pb[h]), absmax(k.ma[h], k.mb[h])));
+    e = scale_exp(2.0f * block_max(v));
+    store_block(tid, k, ldexpf(1.0f, -e));
+    __syncthreads();
+  } else {
+    float v = 0.0f;
+    for (int p = tid; p < npix; p += kBlock) {
+      float4 pa, pb, geo;
+      pixel_entry(p, S, npix, image_size, g, nr_stations, spheroidal, aterms,
+                  sg, pa, pb, geo);
+      v = fmaxf(v, absmax(pa, pb));
+    }
+    e = scale_exp(2.0f * block_max(v));
+  }
+  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
   // B fragments and geometry of pairs [pc0, pc0 + KP): one thread per
   // K-block (2 pairs), writing all 16 column lanes of it.
   auto build = [&](int pc0) {
     for (int q = tid; q < KP / 2; q += kBlock) {
-      float sre[2][4], sim[2][4], dre[2][4], dim[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int b = pc0 + 2 * q + h;
-        float4 geo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-        for (int cr = 0; cr < 4; ++cr)
-          sre[h][cr] = sim[h][cr] = dre[h][cr] = dim[h][cr] = 0.0f;
-        if (b < half) {
-          float4 pa, pb, ma, mb, mgeo;
-          pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
-                      aterms, sg, pa, pb, geo);
-          if constexpr (MIRROR) {
-            pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
-                        spheroidal, aterms, sg, ma, mb, mgeo);
-          } else {
-            ma = mb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          }
-          const float pr[4] = {pa.x, pa.z, pb.x, pb.z};
-          const float pi[4] = {pa.y, pa.w, pb.y, pb.w};
-          const float mr[4] = {ma.x, ma.z, mb.x, mb.z};
-          const float mi[4] = {ma.y, ma.w, mb.y, mb.w};
-#pragma unroll
-          for (int cr = 0; cr < 4; ++cr) {
-            sre[h][cr] = (pr[cr] + mr[cr]) * scale;
-            sim[h][cr] = (pi[cr] + mi[cr]) * scale;
-            dre[h][cr] = (pr[cr] - mr[cr]) * scale;
-            dim[h][cr] = (pi[cr] - mi[cr]) * scale;
-          }
-        }
-        geo_l[2 * q + h] = geo.x;
-        geo_m[2 * q + h] = geo.y;
-        geo_o[2 * q + h] = geo.w;
-        if constexpr (!MIRROR) geo_n[2 * q + h] = geo.z;
-      }
-      // lane (g, col) of K-step ks: ks = q / 4, g = q % 4
-      uint2 *dst = bfr + (q >> 2) * 64 + (q & 3) * 16;
-#pragma unroll
-      for (int cl = 0; cl < 16; ++cl) {
-        const int cr = (cl & 7) >> 1;
-        const bool im = cl & 1;
-        const float bc0 = im ? sim[0][cr] : sre[0][cr];
-        const float bc1 = im ? sim[1][cr] : sre[1][cr];
-        const float bs0 = im ? dre[0][cr] : -dim[0][cr];
-        const float bs1 = im ? dre[1][cr] : -dim[1][cr];
-        dst[cl] = (cl & 8) ? make_uint2(split_lo(bc0, bc1), split_lo(bs0, bs1))
-                           : make_uint2(split_hi(bc0, bc1), split_hi(bs0, bs1));
-      }
+      Block k;
+      entries(pc0, q, k);
+      store_block(q, k, scale);
     }
   };
-  if (single) {
-    build(0);
-    __syncthreads();
-  }
 
   // Chunks of KP pairs are the outermost loop so that building the next
   // chunk never overlaps live accumulators (no spills); each chunk's partial
