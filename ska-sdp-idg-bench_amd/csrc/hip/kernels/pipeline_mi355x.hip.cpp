@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256)
 // grid[z][pol][cy + y][cx + x] += shift_phasor(x, y) * F[s][pol][ys][xs],
 // ys = (y + S/2) % S, xs = (x + S/2) % S.
 //
-// A gather, not a scatter: one workgroup owns one 32 x 32 tile of one
+// A gather, not a scatter: one workgroup owns one 16 x 16 tile of one
 // w-layer, adds the pixels of the subgrids overlapping it into registers in
 // ascending subgrid order and read-modify-writes the tile once.  Every
 // subgrid pixel is read exactly once over the whole launch, there are no
@@ -120,8 +120,14 @@ __global__ void __launch_bounds__(256)
 // bins (count -> scan -> fill, then sorted in LDS); a bin larger than the
 // LDS list falls back to an ordered scan of all the metadata, which yields
 // the same order.
-constexpr int kAddTile = 32;      // grid tile edge (pixels)
-constexpr int kAddPix = 4;        // tile pixels per thread (1024 / 256)
+#ifndef IDG_ADD_TILE
+#define IDG_ADD_TILE 16
+#endif
+#ifndef IDG_ADD_U
+#define IDG_ADD_U 4
+#endif
+constexpr int kAddTile = IDG_ADD_TILE;  // grid tile edge (pixels)
+constexpr int kAddPix = kAddTile * kAddTile / 256;  // tile pixels per thread
 constexpr int kAddMaxTable = 256; // shift phasors kept in LDS for S <= 128
 constexpr int kAddBinCap = 2048;  // bin entries sorted in LDS
 static_assert(kAddTile * kAddTile == 256 * kAddPix, "tile = block x pixels");
@@ -215,7 +221,7 @@ __global__ void __launch_bounds__(256)
   // add the entries [0, total) of the LDS list, in list order; U entries
   // per step with every load issued before the first add (lanes outside an
   // entry's subgrid load its pixel 0 and drop it)
-  constexpr int U = 2;
+  constexpr int U = IDG_ADD_U;
   auto add_list = [&](int total) {
     for (int e = 0; e < total; e += U) {
       float2 v[U][kAddPix][4];
