@@ -36,6 +36,13 @@
 #include "mfma.hpp"
 
 // waves-per-SIMD launch bound of the MFMA degridder (tuning knob)
+// channels per MFMA pass (accumulators per wave) and per phase anchor
+#ifndef IDG_DEGRID_CT
+#define IDG_DEGRID_CT 16
+#endif
+#ifndef IDG_DEGRID_CB
+#define IDG_DEGRID_CB 16
+#endif
 #ifndef IDG_DEGRID_WAVES
 #define IDG_DEGRID_WAVES 4
 #endif
@@ -444,12 +451,12 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
     const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
     __syncthreads();
     if (eligible)
-      degrid_mfma<S_CT, CT, 16, KP, true>(g, S, npix, image_size, C,
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true>(g, S, npix, image_size, C,
                                           nr_stations, uvw, wavenumbers,
                                           visibilities, spheroidal, aterms,
                                           sg, lds);
     else
-      degrid_mfma<S_CT, CT, 16, KP, false>(g, S, npix, image_size, C,
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false>(g, S, npix, image_size, C,
                                            nr_stations, uvw, wavenumbers,
                                            visibilities, spheroidal, aterms,
                                            sg, lds);
@@ -569,7 +576,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
 }
 
 #define IDG_DEGRIDDER(S_, CG_, MODE_) \
-  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_, MODE_, 16>)
+  reinterpret_cast<const void *>(&kernel_degridder_mi355x<S_, CG_, MODE_, IDG_DEGRID_CT>)
 
 // IDG_DEGRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int degridder_impl() {
