@@ -12,6 +12,24 @@ is missing or the counter cannot be read; it never affects the timed path.
 """
 
 
+def _handle_of(amdsmi, handles, device_index):
+    """The amdsmi handle of HIP device `device_index`: matched by PCI
+    domain:bus:device (HIP and amdsmi need not enumerate in the same order,
+    and HIP_VISIBLE_DEVICES renumbers), else by position."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(device_index)
+        want = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+        for h in handles:
+            bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)  # "dddd:bb:dd.f"
+            dom, bus, rest = bdf.split(":")
+            if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                return h
+    except Exception:
+        pass
+    return handles[min(device_index, len(handles) - 1)]
+
+
 class EnergyMeter:
     def __init__(self, device_index=0):
         self.available = False
@@ -25,7 +43,7 @@ class EnergyMeter:
             if not handles:
                 return
             self._smi = amdsmi
-            self._handle = handles[min(device_index, len(handles) - 1)]
+            self._handle = _handle_of(amdsmi, handles, device_index)
             self._read()  # probe once
             self.available = True
         except Exception:
