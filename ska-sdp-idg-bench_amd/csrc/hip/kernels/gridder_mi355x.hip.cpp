@@ -406,10 +406,20 @@ __device__ __forceinline__ void grid_mfma(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                   const float kj = kb[4 * u + j];
+#if IDG_GRID_SCALAR_PHASE
+                  // unpacked: v_pk_*_f32 beside MFMAs can cost more than
+                  // two scalar ops (A/B knob)
+                  floatx2 r;
+                  r.x = fma_(fma_(NP[h].x, kj, PG2[h].x) - A2[h].x, kInv2PiHi,
+                             R2[h].x);
+                  r.y = fma_(fma_(NP[h].y, kj, PG2[h].y) - A2[h].y, kInv2PiHi,
+                             R2[h].y);
+#else
                   const floatx2 ph =
                       __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
                   const floatx2 r =
                       __builtin_elementwise_fma(ph - A2[h], ih, R2[h]);
+#endif
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
