@@ -2,28 +2,35 @@
 """bench.py -- IDG gridder + degridder throughput on MI355X (BASELINE.json metric).
 
 One step = one gridder pass + one degridder pass over one batch of the
-workload, both kernels on the same HIP stream, inputs resident in HBM.  At
-N=1 the batch is BASELINE.json configs[1], the reference's perf defaults
+workload, both kernels on the same HIP stream, inputs resident in HBM.  The
+batch is BASELINE.json configs[1], the reference's perf defaults
 (app/HIP/util.cpp:181-187): NR_STATIONS=50, NR_TIMESLOTS=20,
 NR_TIMESTEPS_SUBGRID=128, NR_CHANNELS=16, SUBGRID_SIZE=32, GRID_SIZE=1024
--> 24,500 subgrids, 50.176 M visibilities, with the reference's own synthetic
-generators (srand(0)).  With N GPUs (one process per GPU, torchrun) every
-rank processes its own batch of that size -- weak scaling, subgrid-sharded,
-no collective on the data path; value = all ranks' visibilities / the max
-over ranks of the timed region.
+-> 24,500 subgrids, 50.176 M visibilities, made by the reference's own
+synthetic generators (srand(0)).
+
+With N GPUs (one process per GPU, torchrun) the ONE batch is sharded
+(BASELINE configs[3]): idg_amd.shard.plan_shards cuts the subgrids into N
+contiguous ranges of equal cost, every rank uploads only its range's
+metadata (rebased), uvw and visibility rows and degridder-input subgrids, and
+grids / degrids just those (3,062-3,063 subgrids per GPU at N = 8).  No
+collective on the data path; `value` = the batch's visibilities / the max
+over ranks of the timed region (strong scaling).  The per-rank full-batch
+(replicated, weak-scaling) figure is measured too and reported beside it as
+`weak_scaling`; `--mode replicated` makes it the headline instead.
 
 `value` counts a visibility once per step (it is gridded AND degridded);
-per-kernel Mvis/s are reported alongside.  The roofline object is for the
-dominant (slower) kernel: achieved = the reference work model's FLOPs per
-launch (app/common/common.cpp:100-129; 35,459 FLOP/vis at this config) /
-that kernel's mean duration from HIP events on its stream; peak = MI355X FP32
-(157.3 TFLOP/s -- vector and f32-MFMA peaks are equal on gfx950).  The path is
-compute-bound; its HBM roofline fraction is reported too.  cpu_baseline times
-the reference's own CPU path (oracle/_ref) on a bounded sample of the same
-batch: on 16 host threads (`value`, disjoint subgrid ranges) and on 1 thread
-as the reference builds it (`single_thread`).
+per-kernel Mvis/s are reported alongside.  `roofline` is for the dominant
+(slower) kernel -- see roofline_for() and DESIGN.md §4.3: the kernels are
+bound by vector-issue cycles (exact phase, v_sin/v_cos, f16 operand split,
+MFMA issue), so `frac` is the measured time's share of that issue ceiling,
+and the f16-MFMA and FP32-equivalent views are reported beside it.
+cpu_baseline times the reference's own CPU path (oracle/_ref) on a bounded
+sample of the same batch, on the host cores this process may use and on one
+thread as the reference builds it.
 
     python bench.py [--gpus N --steps K --warmup W] [--workload default]
+                    [--mode sharded|replicated] [--dump DIR]
 """
 import argparse
 import json
@@ -35,8 +42,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ska-sdp-idg-bench_amd"))
 
 METRIC = "Mvisibilities/s (gridder & degridder) at 1/2/4/8 GPUs; % HBM roofline"
-FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CLOCK_HZ = 2.4e9            # MI355X_MICROARCH.md: max engine clock
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector = FP32 matrix
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA, dense
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Issue cost per wave64 instruction on one SIMD, in cycles at 2.4 GHz
+# (tests/probes/rates_probe.hip, profiles/r01/rates_probe.txt)
+ISSUE_CYC = {"trans": 9.65, "mfma_f16": 8.0, "other": 4.47}
+MFMA_F16_FLOP = 16 * 16 * 32 * 2  # v_mfma_f32_16x16x32_f16
+NR_SIMDS = 1024
 
 WORKLOADS = {
     # BASELINE.json configs[1] (the metric's config)
@@ -55,6 +69,8 @@ WORKLOADS = {
                   nr_channels=16, grid_size=1024, subgrid_size=32,
                   w_range=200.0, w_step=2.5, w_layers=7),
 }
+BASELINE_CONFIG = {"default": "configs[1]", "c256": "configs[2]",
+                   "s64": "configs[4]", "wterm": "SURVEY.md §8f row 4"}
 
 
 def apply_wterms(w, a):
@@ -68,27 +84,137 @@ def apply_wterms(w, a):
     a["metadata"]["z"] = rng.integers(0, w["w_layers"], a["metadata"].size)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="must equal the torchrun world size (1 without it)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="default", choices=sorted(WORKLOADS))
+    ap.add_argument("--mode", default="sharded",
+                    choices=("sharded", "replicated"),
+                    help="sharded: the one batch split over the ranks "
+                         "(strong scaling, BASELINE configs[3]); replicated: "
+                         "every rank processes the whole batch (weak)")
     ap.add_argument("--timeslots", type=int, default=None,
                     help="override NR_TIMESLOTS (batch size)")
-    ap.add_argument("--cpu-sample-subgrids", type=int, default=128)
+    ap.add_argument("--cpu-sample-subgrids", type=int, default=128,
+                    help="subgrids per host thread in the cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the FFT / adder / grid-sum / splitter")
+    ap.add_argument("--no-weak", action="store_true",
+                    help="skip the replicated (weak-scaling) side figure")
+    ap.add_argument("--dump", default=None,
+                    help="rank 0 writes the gathered gridder subgrids, "
+                         "degridded visibilities and summed uv grid here "
+                         "(.npy; tests/test_gpu_dist.py)")
     ap.add_argument("--traffic-file", default=os.path.join(
         REPO, "profiles", "traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# Batch and shards (host side; imported by tests/test_distributed.py)
+# ---------------------------------------------------------------------------
+def workload(name, timeslots=None):
+    w = dict(WORKLOADS[name])
+    if timeslots:
+        w["nr_timeslots"] = timeslots
+    return w
+
+
+def make_batch(w, nthreads=8):
+    """The whole batch on the host: the reference generators (srand(0)),
+    identical on every rank, plus the workload's w-terms."""
+    import idg_amd
+    a = idg_amd.generate(w["nr_stations"], w["nr_timeslots"],
+                         w["nr_timesteps"], w["nr_channels"], w["grid_size"],
+                         w["subgrid_size"], nthreads=nthreads)
+    apply_wterms(w, a)
+    return a
+
+
+def shard_batch(a, rank, world, mode="sharded"):
+    """This rank's part of the batch: subgrid range [s0, s1) of
+    shard.plan_shards, its metadata rebased to its own row space
+    (shard.shard), and ONLY the uvw / visibility rows and degridder-input
+    subgrids that range reads.  Replicated, spheroidal / A-terms /
+    wavenumbers.  mode="replicated" returns the whole batch."""
+    import numpy as np
+    from idg_amd import shard
+    md = a["metadata"]
+    C = a["wavenumbers"].size
+    uvw_rows = a["uvw"].reshape(-1, 3)
+    vis_rows = a["visibilities"].reshape(-1, C, 4, 2)
+    if mode == "replicated" or world == 1:
+        s0, s1 = 0, md.size
+        sub, r0, r1 = shard.shard(md, s0, s1)
+    else:
+        s0, s1 = shard.plan_shards(md, world)[rank]
+        sub, r0, r1 = shard.shard(md, s0, s1)
+    return {
+        "s0": s0, "s1": s1, "row0": r0, "row1": r1,
+        "metadata": sub,
+        "uvw": np.ascontiguousarray(uvw_rows[r0:r1]),
+        "visibilities": np.ascontiguousarray(vis_rows[r0:r1]),
+        "subgrids": np.ascontiguousarray(a["subgrids"][s0:s1]),
+        "wavenumbers": a["wavenumbers"], "spheroidal": a["spheroidal"],
+        "aterms": a["aterms"],
+    }
+
+
+def shard_counts(a, world, mode="sharded"):
+    """Subgrids per rank, in rank order (for gathers)."""
+    from idg_amd import shard
+    if mode == "replicated" or world == 1:
+        return [a["metadata"].size] * world
+    return [s1 - s0 for s0, s1 in shard.plan_shards(a["metadata"], world)]
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (the reference's own CPU path; test infrastructure)
+# ---------------------------------------------------------------------------
+def host_cpus():
+    """The host CPUs this process may use: the affinity mask, capped by a
+    cgroup CPU quota when there is one (on the GPU box `nproc` shows the
+    whole machine while the job gets a share of it)."""
+    import math
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, math.floor(int(q) / int(period)))
+    except Exception:
+        pass
+    info["cgroup_quota"] = quota
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    usable = info["affinity"] or 1
+    if quota:
+        usable = min(usable, quota)
+    info["usable"] = usable
+    return info
 
 
 def cpu_baseline(w, a, nsample):
-    """Time the reference CPU path (oracle/_ref, else the oracle port) on the
-    first `nsample` subgrids of the batch.  Test infrastructure only: the
-    baseline the GPU number is reported beside, never the measured path."""
+    """Time the reference CPU path (oracle/_ref, else the oracle port) on
+    a bounded sample of the batch: on every usable host core (`value`) and
+    on one thread as the reference builds it (`single_thread`).  Test
+    infrastructure only: the baseline the GPU number is reported beside,
+    never the measured path."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc
@@ -126,26 +252,28 @@ def cpu_baseline(w, a, nsample):
         "gridder_mvis_s": round(nvis / (t1 - t0) / 1e6, 4),
         "degridder_mvis_s": round(nvis / (t2 - t1) / 1e6, 4),
     }
-    multi = cpu_baseline_threads(w, a, impl, kind, args, nsample, extra)
+    cpus = host_cpus()
+    multi = cpu_baseline_threads(w, a, impl, kind, args, nsample, extra,
+                                 cpus["usable"])
     out = dict(multi or single)
-    out.update({"unit": "Mvis/s", "kind": kind})
+    out.update({"unit": "Mvis/s", "kind": kind, "host": cpus})
     if multi:
         out["single_thread"] = single
     return out
 
 
-def cpu_baseline_threads(w, a, impl, kind, args, nsample, extra):
-    """The same CPU path on `cores` host threads (the GPU box's CPU share),
-    each thread running the reference's own kernel on its own contiguous
-    range of `nsample` subgrids (ctypes drops the GIL during the call).  The
-    ranges write disjoint subgrids / visibility rows.  Only valid when every
-    subgrid has the same baseline_offset (the kernels rebase row indices on
-    metadata[0].baseline_offset, gridder_reference.cpp:16-25) -- true for the
-    synthetic batch; otherwise None."""
+def cpu_baseline_threads(w, a, impl, kind, args, nsample, extra, cores):
+    """The same CPU path on `cores` host threads, each running the
+    reference's own kernel on its own contiguous range of `nsample`
+    subgrids (ctypes drops the GIL during the call).  The ranges write
+    disjoint subgrids / visibility rows.  Only valid when every subgrid has
+    the same baseline_offset (the kernels rebase row indices on
+    metadata[0].baseline_offset, gridder_reference.cpp:16-25) -- true for
+    the synthetic batch; otherwise None."""
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     md_all = a["metadata"]
-    cores = int(os.environ.get("IDG_CPU_BASELINE_THREADS", "16"))
+    cores = int(os.environ.get("IDG_CPU_BASELINE_THREADS", cores))
     n = min(nsample * cores, md_all.size)
     if cores < 2 or n < 2 * cores or np.any(
             md_all["baseline_offset"][:n] != md_all["baseline_offset"][0]):
@@ -193,21 +321,444 @@ def cpu_baseline_threads(w, a, impl, kind, args, nsample, extra):
     }
 
 
-def traffic_for(path, workload, kernel):
+# ---------------------------------------------------------------------------
+# Committed profile data (profiles/traffic.json)
+# ---------------------------------------------------------------------------
+def profile_entry(path, workload_name, kernel):
     try:
         with open(path) as f:
-            t = json.load(f)
-        return t[workload][kernel]["hbm_bytes_per_launch"]
+            return json.load(f)[workload_name][kernel]
     except Exception:
         return None
 
 
-def reference_hip_for(workload, sec_per_step, t_grid, t_degrid):
+def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled):
+    """Roofline of the dominant kernel.
+
+    The kernels are bound by vector issue: per phasor, the exact fp32 phase,
+    v_sin + v_cos, the two-term f16 split of the MFMA operand and half an
+    f16 MFMA, all issued by the same SIMD.  The ceiling is the time the
+    kernel's own instruction stream needs at full issue rate:
+        t_issue = (trans x 9.65 + mfma_f16 x 8 + other VALU x 4.47) cycles
+                  / 1024 SIMDs / 2.4 GHz
+    from the per-launch wave-instruction counts of the committed SQ profile
+    (profiles/traffic.json -> issue_bound; scaled by subgrids when this
+    launch grids a shard) and the measured issue costs
+    (tests/probes/rates_probe.hip).  achieved = the reference work model's
+    FLOPs (app/common/common.cpp:100-129) / measured time; peak = the same
+    FLOPs / t_issue; frac = t_issue / t <= 1.  Beside it: executed f16 MFMA
+    FLOP/s against the dense f16 peak (mfma), and the work model against the
+    FP32 peak the reference prices it on (fp32_equivalent; > 1 because the
+    complex MAC runs on the f16 matrix core)."""
+    achieved = flops / t / 1e12
+    out = {"bound": "mfma", "achieved": round(achieved, 3),
+           "unit": "TFLOP/s", "kernel": kernel,
+           "traffic": None}
+    ib = (entry or {}).get("issue_bound")
+    scale = nsub_launch / nsub_profiled if nsub_profiled else 1.0
+    if entry and entry.get("hbm_bytes_per_launch"):
+        out["traffic"] = int(entry["hbm_bytes_per_launch"] * scale)
+    if ib and ib.get("insts_valu"):
+        trans = ib["insts_trans"] * scale
+        mfma = ib["insts_mfma_f16"] * scale
+        other = ib["insts_valu"] * scale - trans - mfma
+        cyc = (trans * ISSUE_CYC["trans"] + mfma * ISSUE_CYC["mfma_f16"] +
+               other * ISSUE_CYC["other"]) / NR_SIMDS
+        t_issue = cyc / CLOCK_HZ
+        peak = flops / t_issue / 1e12
+        out.update({
+            "resource": "vector issue per SIMD (v_sin/v_cos + VALU + f16 "
+                        "MFMA issue cycles of the kernel's own instruction "
+                        "stream)",
+            "peak": round(peak, 3),
+            "frac": round(t_issue / t, 4),
+            "issue_model": {
+                "t_issue_ms": round(t_issue * 1e3, 4),
+                "insts_per_launch": {"trans": trans, "mfma_f16": mfma,
+                                     "other_valu": other},
+                "cycles": ISSUE_CYC, "clock_ghz": CLOCK_HZ / 1e9,
+                "source": ib.get("source"),
+            },
+        })
+        mfma_tf = mfma * MFMA_F16_FLOP / t / 1e12
+        out["mfma"] = {"achieved": round(mfma_tf, 3),
+                       "peak": F16_MFMA_PEAK_TFLOPS,
+                       "frac": round(mfma_tf / F16_MFMA_PEAK_TFLOPS, 4),
+                       "note": "executed v_mfma_f32_16x16x32_f16 FLOPs "
+                               "(two-term split: 4 f16 products per f32 "
+                               "MAC) / measured time"}
+    else:
+        # no committed counters for this workload: the dense f16 MFMA peak
+        out.update({"peak": F16_MFMA_PEAK_TFLOPS,
+                    "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
+                    "resource": "f16 MFMA dense peak (no SQ profile of this "
+                                "workload committed)"})
+    out["fp32_equivalent"] = {
+        "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+        "ratio": round(achieved / FP32_PEAK_TFLOPS, 4),
+        "note": "the reference work model priced on the FP32 peak; > 1 "
+                "because its complex MAC runs on the f16 matrix core"}
+    out["note"] = (f"achieved = reference work model {flops / nvis:.0f} "
+                   f"FLOP/vis x {nvis} vis per launch / mean kernel duration "
+                   "(HIP events on the launch stream); frac = issue-model "
+                   "time / measured time (DESIGN.md §4.3)")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Timed run
+# ---------------------------------------------------------------------------
+def upload(part):
+    import numpy as np
+    import torch
+    dev = {k: torch.from_numpy(part[k]).cuda() for k in
+           ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms",
+            "subgrids")}
+    dev["metadata"] = torch.from_numpy(
+        part["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
+    return dev
+
+
+def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None):
+    """warmup untimed steps, then `steps` timed ones bracketed by barrier +
+    synchronize.  Returns (elapsed max over ranks, t_grid, t_degrid (mean
+    per launch, max over ranks), joules, outputs)."""
+    import torch
+    import idg_amd
+    S, C, G = w["subgrid_size"], w["nr_channels"], w["grid_size"]
+    p = (nsub, G, S, idg_amd.IMAGE_SIZE, w.get("w_step", idg_amd.W_STEP), C,
+         w["nr_stations"])
+    grid_out = torch.empty_like(dev["subgrids"])
+    degrid_out = torch.empty_like(dev["visibilities"])
+
+    def step(ev=None):
+        if nsub == 0:
+            return
+        if ev:
+            ev[0].record(stream)
+        idg_amd.gridder_launch(*p, dev["uvw"], dev["wavenumbers"],
+                               dev["visibilities"], dev["spheroidal"],
+                               dev["aterms"], dev["metadata"], grid_out,
+                               stream=stream)
+        if ev:
+            ev[1].record(stream)
+        idg_amd.degridder_launch(*p, dev["uvw"], dev["wavenumbers"],
+                                 degrid_out, dev["spheroidal"], dev["aterms"],
+                                 dev["metadata"], dev["subgrids"],
+                                 stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for _ in range(steps)]
+    dist.barrier()
+    torch.cuda.synchronize()
+    if meter:
+        meter.start()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    joules = meter.stop() if meter else None
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = dist.max_over_ranks(elapsed)
+    if nsub:
+        t_grid = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+        t_degrid = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
+    else:
+        t_grid = t_degrid = 0.0
+    return (elapsed_max, dist.max_over_ranks(t_grid),
+            dist.max_over_ranks(t_degrid), joules, elapsed,
+            (grid_out, degrid_out))
+
+
+def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
+    """Gridder output -> FFT -> adder -> grid-sum over ranks and splitter ->
+    FFT: the IDG steps either side of the path (not in `value`).  Returns
+    (timings dict, the summed grid of the last pass)."""
+    import torch
+    import idg_amd
+    G, S = w["grid_size"], w["subgrid_size"]
+    nw = w.get("w_layers", 1)
+    gridt = torch.zeros((nw, 4, G, G, 2), dtype=torch.float32, device="cuda")
+    uvsub = torch.empty_like(sub_out)
+    npipe = max(1, min(steps, 5))
+    pev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)]
+           for _ in range(npipe)]
+    has = sub_out.shape[0] > 0
+    for it in range(npipe + 1):
+        e = pev[it - 1] if it > 0 else None
+        uvsub.copy_(sub_out)
+        gridt.zero_()
+        dist.barrier()
+        if e:
+            e[0].record(stream)
+        if has:
+            idg_amd.subgrid_fft_launch(uvsub, +1, 1.0, stream=stream)
+        if e:
+            e[1].record(stream)
+        if has:
+            idg_amd.adder_launch(G, dev["metadata"], uvsub, gridt,
+                                 nr_w_layers=nw, stream=stream)
+        if e:
+            e[2].record(stream)
+        dist.reduce_grid(gridt)
+        if e:
+            e[3].record(stream)
+        if has:
+            idg_amd.splitter_launch(G, dev["metadata"], gridt, uvsub,
+                                    nr_w_layers=nw, stream=stream)
+        if e:
+            e[4].record(stream)
+        if has:
+            idg_amd.subgrid_fft_launch(uvsub, -1, 1.0 / (S * S),
+                                       stream=stream)
+        if e:
+            e[5].record(stream)
+    torch.cuda.synchronize()
+
+    def avg(i, j):
+        return dist.max_over_ranks(
+            sum(e[i].elapsed_time(e[j]) for e in pev) / npipe)
+    out = {
+        "fft_ms": round(avg(0, 1), 4),
+        "adder_ms": round(avg(1, 2), 4),
+        "grid_reduce_ms": round(avg(2, 3), 4),
+        "splitter_ms": round(avg(3, 4), 4),
+        "ifft_ms": round(avg(4, 5), 4),
+        "grid": (f"[{nw}][4][{G}][{G}] complex64, "
+                 f"{nw * G * G * 32 / 2**20:.0f} MiB"),
+        "grid_reduce": (f"all_reduce(sum) of the ranks' partial grids, "
+                        f"{dist.backend_name()}"
+                        if world > 1 else "single rank: no collective"),
+    }
+    return out, gridt
+
+
+def main(argv=None):
+    args = parse(argv)
+    import numpy as np
+    import torch
+    import idg_amd
+    from idg_amd import dist
+
+    rank, local_rank, world = dist.init()
+    if args.gpus != world:
+        raise SystemExit(
+            f"bench.py: --gpus {args.gpus} but the world size is {world}; "
+            "launch N>1 under torchrun (--nproc-per-node N)")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    w = workload(args.workload, args.timeslots)
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+
+    # ---- synthetic batch (reference generators), this rank's part in HBM --
+    threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    a = make_batch(w, nthreads=threads)
+    ns_total = a["metadata"].size
+    idg_amd.validate_metadata(ns_total, S, C, w["nr_stations"], ns_total * T,
+                              w["nr_timeslots"], a["metadata"])
+    part = shard_batch(a, rank, world, args.mode)
+    nsub = part["s1"] - part["s0"]
+    idg_amd.validate_metadata(nsub, S, C, w["nr_stations"],
+                              part["row1"] - part["row0"],
+                              w["nr_timeslots"], part["metadata"])
+    dev = upload(part)
+    stream = torch.cuda.current_stream()
+
+    from idg_amd.energy import EnergyMeter
+    meter = EnergyMeter(local_rank)
+    elapsed_max, t_grid, t_degrid, joules, elapsed, outs = time_steps(
+        w, dev, nsub, args.steps, args.warmup, stream, dist, meter)
+    sec_per_step = elapsed_max / args.steps
+    # visibilities processed per step by all ranks together
+    nvis_job = (ns_total * T * C * (world if args.mode == "replicated" else 1))
+    nvis_rank = nsub * T * C
+    nvis_max = dist.max_over_ranks(nvis_rank)  # the busiest rank's share
+    nsub_max = int(nvis_max // (T * C))
+
+    flops = idg_amd.flops_gridder(C, nsub_max * T, nsub_max, S)
+    nbytes = idg_amd.bytes_gridder(C, nsub_max * T, nsub_max, S)
+    kernels = {}
+    for name, t in (("gridder", t_grid), ("degridder", t_degrid)):
+        kname = idg_amd.kernel_name(name, S, C)
+        kernels[name] = {
+            "kernel": kname,
+            "ms": round(t * 1e3, 4),
+            "mvis_s_per_gpu": round(nvis_max / t / 1e6, 2),
+            "tflops": round(flops / t / 1e12, 3),
+            "hbm_gbs_model": round(nbytes / t / 1e9, 2),
+        }
+    dom = "gridder" if t_grid >= t_degrid else "degridder"
+    t_dom = t_grid if dom == "gridder" else t_degrid
+    entry = profile_entry(args.traffic_file, args.workload,
+                          kernels[dom]["kernel"])
+    roofline = roofline_for(entry, kernels[dom]["kernel"], flops, nvis_max,
+                            t_dom, nsub_max, ns_total if entry else 0)
+    if entry and entry.get("algorithmic_bytes"):
+        roofline["algorithmic_bytes"] = int(
+            entry["algorithmic_bytes"] * nsub_max / ns_total)
+    roofline_hbm = {
+        "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+        "achieved": round(nbytes / t_dom / 1e9, 2),
+        "frac": round(nbytes / t_dom / 1e9 / HBM_PEAK_GBS, 4),
+        "note": ("reference byte model (common.cpp:131-159, "
+                 f"{nbytes / max(1, nvis_max):.2f} B/vis) over the measured "
+                 f"time; AI = {flops / max(1, nbytes):.0f} FLOP/B, so the "
+                 "path is compute-bound: at this kernel time the HBM "
+                 f"fraction is {nbytes / t_dom / 1e9 / HBM_PEAK_GBS:.3f}"),
+    }
+    if roofline.get("traffic"):
+        roofline_hbm["counter_gbs"] = round(roofline["traffic"] / t_dom / 1e9,
+                                            2)
+
+    # ---- pipeline steps around the path (not in `value`) ----------------
+    pipeline, grid_sum = None, None
+    if not args.no_pipeline or args.dump:
+        pipeline, grid_sum = time_pipeline(w, dev, outs[0], stream,
+                                           args.steps, world, dist)
+        extra = sum(pipeline[k] for k in ("fft_ms", "adder_ms",
+                                          "grid_reduce_ms", "splitter_ms",
+                                          "ifft_ms")) / 1e3
+        pipeline["full_cycle_mvis_s"] = round(
+            nvis_job / (sec_per_step + extra) / 1e6, 2)
+        pipeline["note"] = ("gridder -> FFT -> adder -> grid-sum over ranks "
+                            "and splitter -> FFT around the timed step; "
+                            "reported beside `value`, not in it")
+
+    if args.dump:
+        dump_outputs(args.dump, a, part, outs, grid_sum, rank, world,
+                     args.mode, dist)
+
+    # ---- energy over the timed region (amdsmi accumulated-energy counter;
+    # the reference's PowerSensor report, app/HIP/util.cpp:134-159) --------
+    energy = None
+    if joules is not None and joules > 0:
+        j_all = dist.sum_over_ranks(joules)
+        energy = {
+            "joules_per_step": round(j_all / args.steps, 4),
+            "avg_power_w_per_gpu": round(j_all / world / elapsed, 1),
+            "mvis_per_joule": round(nvis_job * args.steps / j_all / 1e6, 3),
+            "source": "amdsmi_get_energy_count over the timed steps",
+        }
+
+    # ---- the other scaling mode, beside the headline ----------------------
+    weak = None
+    if world > 1 and args.mode == "sharded" and not args.no_weak:
+        del dev, outs
+        torch.cuda.empty_cache()
+        full = upload(shard_batch(a, rank, world, "replicated"))
+        wsteps = max(1, min(args.steps, 5))
+        w_el, w_tg, w_td, _, _, _ = time_steps(
+            w, full, ns_total, wsteps, 1, stream, dist)
+        weak = {
+            "value": round(world * ns_total * T * C * wsteps / w_el / 1e6, 2),
+            "ms_per_step": round(w_el / wsteps * 1e3, 4),
+            "nr_subgrids_per_gpu": ns_total,
+            "gridder_ms": round(w_tg * 1e3, 4),
+            "degridder_ms": round(w_td * 1e3, 4),
+            "steps": wsteps,
+            "note": "every rank processes the whole batch (replicated); "
+                    "value = all ranks' visibilities / max over ranks",
+        }
+
+    sharded = args.mode == "sharded" and world > 1
+    result = {
+        "metric": METRIC,
+        "value": round(nvis_job / sec_per_step / 1e6, 2),
+        "unit": "Mvis/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(sec_per_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if args.mode == "replicated" else "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference generators app/common/init.cpp, srand(0))",
+        "config": {
+            "workload": (f"{args.workload}: NR_STATIONS={w['nr_stations']} "
+                         f"NR_TIMESLOTS={w['nr_timeslots']} "
+                         f"NR_TIMESTEPS_SUBGRID={T} NR_CHANNELS={C} "
+                         f"SUBGRID_SIZE={S} GRID_SIZE={w['grid_size']}"
+                         + (f" W_STEP={w['w_step']} w~U(-{w['w_range']:g},"
+                            f"{w['w_range']:g}) w-layers={w['w_layers']}"
+                            if w.get("w_range") else "")),
+            "baseline_config": (("configs[3] (configs[1] sharded)"
+                                 if sharded else
+                                 BASELINE_CONFIG[args.workload])
+                                if args.workload == "default"
+                                else BASELINE_CONFIG[args.workload]),
+            "nr_subgrids": ns_total,
+            "nr_subgrids_per_gpu": shard_counts(a, world, args.mode),
+            "visibilities_per_step": nvis_job,
+            "step": "gridder + degridder over the batch",
+            "parallelism": (f"subgrid-sharded x{world} (contiguous equal-cost "
+                            "ranges, idg_amd.shard), no data-path collective"
+                            if args.mode == "sharded" else
+                            f"replicated x{world} (each rank the whole "
+                            "batch), no data-path collective"),
+        },
+        "gridder_mvis_s": round(nvis_job / t_grid / 1e6, 2),
+        "degridder_mvis_s": round(nvis_job / t_degrid / 1e6, 2),
+        "kernels": kernels,
+        "roofline": roofline,
+        "roofline_hbm": roofline_hbm,
+        "weak_scaling": weak,
+        "pipeline": pipeline,
+        "energy": energy,
+        "reference_hip_mi355x": (reference_hip_for(
+            args.workload, sec_per_step, t_grid, t_degrid)
+            if world == 1 else None),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w, a, args.cpu_sample_subgrids)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.finalize()
+    return result
+
+
+def dump_outputs(path, a, part, outs, grid_sum, rank, world, mode, dist):
+    """Gather the ranks' gridder subgrids and degridded visibility rows in
+    rank order (they are disjoint) and write them with the summed uv grid
+    from rank 0 (tests/test_gpu_dist.py compares N ranks with one)."""
+    import numpy as np
+    counts = shard_counts(a, world, mode)
+    T = a["uvw"].shape[1]
+    cpu = not dist.collectives_on_device()
+    sub = outs[0].cpu() if cpu else outs[0]
+    vis = outs[1].reshape(-1, T, *outs[1].shape[1:])
+    vis = vis.cpu() if cpu else vis
+    if mode == "replicated":
+        counts = [counts[0]] + [0] * (world - 1)
+        if rank:
+            sub, vis = sub[:0], vis[:0]
+    all_sub = dist.gather_shards(sub, counts)
+    all_vis = dist.gather_shards(vis, counts)
+    if rank == 0:
+        os.makedirs(path, exist_ok=True)
+        np.save(os.path.join(path, "subgrids.npy"), all_sub.cpu().numpy())
+        np.save(os.path.join(path, "visibilities.npy"),
+                all_vis.cpu().numpy())
+        if grid_sum is not None:
+            np.save(os.path.join(path, "grid.npy"), grid_sum.cpu().numpy())
+        with open(os.path.join(path, "meta.json"), "w") as f:
+            json.dump({"world": world, "mode": mode, "counts": counts}, f)
+
+
+def reference_hip_for(workload_name, sec_per_step, t_grid, t_degrid):
     """The reference's own HIP kernels measured on MI355X at configs[1]
     (profiles/reference_hip.json, made by tests/debug/ref_hip.sh): this
     run's per-GPU rates over theirs, for the fastest reference kernels and
     for the fastest that pass the reference's own -c check."""
-    if workload != "default":
+    if workload_name != "default":
         return None
     try:
         with open(os.path.join(REPO, "profiles", "reference_hip.json")) as f:
@@ -228,266 +779,6 @@ def reference_hip_for(workload, sec_per_step, t_grid, t_degrid):
             "speedup_degridder": round(r["degridder_ms"] / 1e3 / t_degrid, 2),
         }
     return out
-
-
-def issue_for(path, workload, kernel):
-    """VALU-issue utilisation of a kernel from its committed PMC summary."""
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        return t[workload][kernel].get("issue_bound")
-    except Exception:
-        return None
-
-
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import idg_amd
-    from idg_amd import dist
-
-    rank, local_rank, world = dist.init()
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
-    torch.cuda.set_device(local_rank)
-    w = dict(WORKLOADS[args.workload])
-    if args.timeslots:
-        w["nr_timeslots"] = args.timeslots
-    st, ts, T, C, G, S = (w["nr_stations"], w["nr_timeslots"],
-                          w["nr_timesteps"], w["nr_channels"], w["grid_size"],
-                          w["subgrid_size"])
-    ns = idg_amd.nr_subgrids_for(st, ts)
-    nvis = ns * T * C
-
-    # ---- synthetic batch (reference generators), resident in HBM ----------
-    threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
-    a = idg_amd.generate(st, ts, T, C, G, S, nthreads=threads)
-    apply_wterms(w, a)
-    idg_amd.validate_metadata(ns, S, C, st, ns * T, ts, a["metadata"])
-    dev = {k: torch.from_numpy(a[k]).cuda() for k in
-           ("uvw", "wavenumbers", "visibilities", "spheroidal", "aterms",
-            "subgrids")}
-    dev["metadata"] = torch.from_numpy(
-        a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
-    grid_out = torch.empty_like(dev["subgrids"])
-    degrid_out = torch.empty_like(dev["visibilities"])
-    p = (ns, G, S, idg_amd.IMAGE_SIZE, w.get("w_step", idg_amd.W_STEP), C,
-         st)
-    stream = torch.cuda.current_stream()
-
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        idg_amd.gridder_launch(*p, dev["uvw"], dev["wavenumbers"],
-                               dev["visibilities"], dev["spheroidal"],
-                               dev["aterms"], dev["metadata"], grid_out,
-                               stream=stream)
-        if ev:
-            ev[1].record(stream)
-        idg_amd.degridder_launch(*p, dev["uvw"], dev["wavenumbers"],
-                                 degrid_out, dev["spheroidal"], dev["aterms"],
-                                 dev["metadata"], dev["subgrids"],
-                                 stream=stream)
-        if ev:
-            ev[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
-              for _ in range(args.steps)]
-    from idg_amd.energy import EnergyMeter
-    meter = EnergyMeter(local_rank)
-    dist.barrier()
-    torch.cuda.synchronize()
-    meter.start()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize()
-    joules = meter.stop()
-    dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed_max = dist.max_over_ranks(elapsed)
-
-    t_grid = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3
-    t_degrid = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps / 1e3
-    t_grid = dist.max_over_ranks(t_grid)
-    t_degrid = dist.max_over_ranks(t_degrid)
-    sec_per_step = elapsed_max / args.steps
-
-    flops = idg_amd.flops_gridder(C, ns * T, ns, S)
-    nbytes = idg_amd.bytes_gridder(C, ns * T, ns, S)
-    kernels = {}
-    for name, t in (("gridder", t_grid), ("degridder", t_degrid)):
-        kname = idg_amd.kernel_name(name, S, C)
-        kernels[name] = {
-            "kernel": kname,
-            "ms": round(t * 1e3, 4),
-            "mvis_s_per_gpu": round(nvis / t / 1e6, 2),
-            "tflops": round(flops / t / 1e12, 3),
-            "fp32_frac": round(flops / t / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "hbm_gbs_model": round(nbytes / t / 1e9, 2),
-        }
-    dom = "gridder" if t_grid >= t_degrid else "degridder"
-    t_dom = t_grid if dom == "gridder" else t_degrid
-    achieved = flops / t_dom / 1e12
-    roofline = {
-        "bound": "mfma",
-        "achieved": round(achieved, 3),
-        "peak": FP32_PEAK_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-        "traffic": traffic_for(args.traffic_file, args.workload,
-                               kernels[dom]["kernel"]),
-        "kernel": kernels[dom]["kernel"],
-        "note": ("achieved = reference work model FLOPs per launch "
-                 f"({flops / nvis:.0f} FLOP/vis x {nvis} vis) / mean "
-                 "kernel duration (HIP events on the launch stream); peak = "
-                 "gfx950 FP32 peak (vector = f32 MFMA = 157.3 TF), the "
-                 "ceiling of the work model as the reference computes it. "
-                 "frac > 1 is possible: the complex MAC (32 of the model's "
-                 "~35 FLOP per pixel-visibility) runs on the f16 matrix "
-                 "core with a two-term f16 split at f32 accuracy, so the "
-                 "binding resource is VALU issue (exact phase, v_sin/v_cos, "
-                 "split), see issue_bound"),
-    }
-    issue = issue_for(args.traffic_file, args.workload,
-                      kernels[dom]["kernel"])
-    if issue is not None:
-        roofline["issue_bound"] = issue
-    roofline_hbm = {
-        "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-        "achieved": round(nbytes / t_dom / 1e9, 2),
-        "frac": round(nbytes / t_dom / 1e9 / HBM_PEAK_GBS, 4),
-        "note": ("reference byte model (common.cpp:131-159, "
-                 f"{nbytes / nvis:.2f} B/vis); AI = {flops / nbytes:.0f} "
-                 "FLOP/B, so <= ~5.5% by construction"),
-    }
-
-    # ---- pipeline steps around the path (not in `value`): subgrid FFT,
-    # adder onto the uv grid, the multi-GPU grid-sum over RCCL (the one
-    # exchange step, BASELINE configs[3]), splitter, inverse FFT ----------
-    pipeline = None
-    if not args.no_pipeline:
-        nw = w.get("w_layers", 1)
-        gridt = torch.zeros((nw, 4, G, G, 2), dtype=torch.float32,
-                            device="cuda")
-        uvsub = torch.empty_like(grid_out)
-        npipe = max(1, min(args.steps, 5))
-        pev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)]
-               for _ in range(npipe)]
-        for it in range(npipe + 1):
-            e = pev[it - 1] if it > 0 else None
-            uvsub.copy_(grid_out)
-            gridt.zero_()
-            dist.barrier()
-            if e:
-                e[0].record(stream)
-            idg_amd.subgrid_fft_launch(uvsub, +1, 1.0, stream=stream)
-            if e:
-                e[1].record(stream)
-            idg_amd.adder_launch(G, dev["metadata"], uvsub, gridt,
-                                 nr_w_layers=nw, stream=stream)
-            if e:
-                e[2].record(stream)
-            dist.reduce_grid(gridt)
-            if e:
-                e[3].record(stream)
-            idg_amd.splitter_launch(G, dev["metadata"], gridt, uvsub,
-                                    nr_w_layers=nw, stream=stream)
-            if e:
-                e[4].record(stream)
-            idg_amd.subgrid_fft_launch(uvsub, -1, 1.0 / (S * S),
-                                       stream=stream)
-            if e:
-                e[5].record(stream)
-        torch.cuda.synchronize()
-
-        def avg(i, j):
-            return dist.max_over_ranks(
-                sum(e[i].elapsed_time(e[j]) for e in pev) / npipe)
-        pipeline = {
-            "fft_ms": round(avg(0, 1), 4),
-            "adder_ms": round(avg(1, 2), 4),
-            "grid_reduce_ms": round(avg(2, 3), 4),
-            "splitter_ms": round(avg(3, 4), 4),
-            "ifft_ms": round(avg(4, 5), 4),
-            "grid": (f"[{nw}][4][{G}][{G}] complex64, "
-                     f"{nw * G * G * 32 / 2**20:.0f} MiB"),
-            "grid_reduce": (f"all_reduce(sum), {dist.backend_name()}"
-                            if world > 1 else "single rank: no collective"),
-        }
-        extra = sum(pipeline[k] for k in ("fft_ms", "adder_ms",
-                                          "grid_reduce_ms", "splitter_ms",
-                                          "ifft_ms")) / 1e3
-        pipeline["full_cycle_mvis_s"] = round(
-            world * nvis / (sec_per_step + extra) / 1e6, 2)
-        pipeline["note"] = ("gridder -> FFT -> adder -> grid-sum and "
-                            "splitter -> FFT -> degridder around the timed "
-                            "step; reported beside `value`, not in it")
-
-    # ---- energy over the timed region (amdsmi accumulated-energy counter;
-    # the reference's PowerSensor report, app/HIP/util.cpp:134-159) --------
-    energy = None
-    if joules is not None and joules > 0:
-        j_all = dist.sum_over_ranks(joules)
-        energy = {
-            "joules_per_step": round(j_all / args.steps, 4),
-            "avg_power_w_per_gpu": round(j_all / world / elapsed, 1),
-            "mvis_per_joule": round(world * nvis * args.steps / j_all / 1e6,
-                                    3),
-            "source": "amdsmi_get_energy_count over the timed steps",
-        }
-
-    result = {
-        "metric": METRIC,
-        "value": round(world * nvis / sec_per_step / 1e6, 2),
-        "unit": "Mvis/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(sec_per_step * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (reference generators app/common/init.cpp, srand(0))",
-        "config": {
-            "workload": (f"{args.workload}: NR_STATIONS={st} "
-                         f"NR_TIMESLOTS={ts} NR_TIMESTEPS_SUBGRID={T} "
-                         f"NR_CHANNELS={C} SUBGRID_SIZE={S} GRID_SIZE={G}"
-                         + (f" W_STEP={w['w_step']} w~U(-{w['w_range']:g},"
-                            f"{w['w_range']:g}) w-layers={w['w_layers']}"
-                            if w.get("w_range") else "")),
-            "baseline_config": ("configs[1]" if args.workload == "default"
-                                else {"c256": "configs[2]",
-                                      "s64": "configs[4]",
-                                      "wterm": "SURVEY.md §8f row 4"}[
-                                          args.workload]),
-            "nr_subgrids_per_gpu": ns,
-            "visibilities_per_gpu_per_step": nvis,
-            "step": "gridder + degridder over the batch",
-            "parallelism": f"subgrid-sharded x{world}, no data-path collective",
-        },
-        "gridder_mvis_s": round(world * nvis / t_grid / 1e6, 2),
-        "degridder_mvis_s": round(world * nvis / t_degrid / 1e6, 2),
-        "kernels": kernels,
-        "roofline": roofline,
-        "roofline_hbm": roofline_hbm,
-        "pipeline": pipeline,
-        "energy": energy,
-        "reference_hip_mi355x": reference_hip_for(
-            args.workload, sec_per_step, t_grid, t_degrid),
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(w, a, args.cpu_sample_subgrids)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    dist.finalize()
 
 
 if __name__ == "__main__":

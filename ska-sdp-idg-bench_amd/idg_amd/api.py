@@ -196,14 +196,57 @@ def _stream_handle(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
+def _dev_extents(nr_subgrids, subgrid_size, nr_channels, nr_stations, uvw,
+                 wavenumbers, visibilities, spheroidal, aterms, metadata,
+                 subgrids, validate):
+    """Host-side shape checks of a device launch (no device access): every
+    tensor must hold exactly the extents the kernel's grid will index.
+    With validate=True the metadata is also copied to the host once and
+    checked against those extents (idg_validate_metadata: row ranges,
+    A-term slots, stations); launches stay asynchronous otherwise, so
+    callers that build their own metadata validate it once up front."""
+    S, C = subgrid_size, nr_channels
+    if uvw.numel() % 3:
+        raise ValueError("uvw must hold whole (u, v, w) triplets")
+    rows = uvw.numel() // 3
+    if visibilities.numel() != rows * C * 8:
+        raise ValueError(
+            f"visibilities must hold uvw rows x nr_channels x 4 complex "
+            f"({rows} x {C} x 4), got {visibilities.numel() // 2}")
+    if wavenumbers.numel() < C:
+        raise ValueError(f"wavenumbers must hold nr_channels ({C}) values")
+    if spheroidal.numel() != S * S:
+        raise ValueError(f"spheroidal must be [{S}][{S}]")
+    per_slot = nr_stations * S * S * 8
+    if aterms.numel() == 0 or aterms.numel() % per_slot:
+        raise ValueError("aterms must be [slots][nr_stations][S][S][4] "
+                         "complex")
+    if metadata.numel() * metadata.element_size() != nr_subgrids * 36:
+        raise ValueError(f"metadata must hold nr_subgrids ({nr_subgrids}) "
+                         "x 36-byte records")
+    if subgrids.numel() != nr_subgrids * 4 * S * S * 2:
+        raise ValueError(f"subgrids must be [{nr_subgrids}][4][{S}][{S}] "
+                         "complex")
+    if validate:
+        md = metadata.detach().cpu().contiguous().view(-1).numpy()
+        validate_metadata(nr_subgrids, S, C, nr_stations, rows,
+                          aterms.numel() // per_slot,
+                          np.frombuffer(md.tobytes(), METADATA_DTYPE))
+
+
 def gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
                    w_step_in_lambda, nr_channels, nr_stations, uvw,
                    wavenumbers, visibilities, spheroidal, aterms, metadata,
-                   subgrids, stream=None):
+                   subgrids, stream=None, validate=False):
     """Enqueue the gridder on device-resident tensors (metadata as int32
-    [NS, 9] tensor or uint8 view of METADATA_DTYPE); returns immediately."""
+    [NS, 9] tensor or uint8 view of METADATA_DTYPE); returns immediately.
+    Tensor extents are checked on the host; validate=True also checks the
+    metadata (one device-to-host copy)."""
     import torch
     f32 = torch.float32
+    _dev_extents(nr_subgrids, subgrid_size, nr_channels, nr_stations, uvw,
+                 wavenumbers, visibilities, spheroidal, aterms, metadata,
+                 subgrids, validate)
     _check(lib.idg_gridder_launch(
         nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
         nr_channels, nr_stations, _dev_ptr(uvw, "uvw", f32),
@@ -218,10 +261,14 @@ def gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
 def degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
                      w_step_in_lambda, nr_channels, nr_stations, uvw,
                      wavenumbers, visibilities, spheroidal, aterms, metadata,
-                     subgrids, stream=None):
-    """Enqueue the degridder on device-resident tensors; returns immediately."""
+                     subgrids, stream=None, validate=False):
+    """Enqueue the degridder on device-resident tensors; returns immediately.
+    Extent checks and `validate` as for gridder_launch."""
     import torch
     f32 = torch.float32
+    _dev_extents(nr_subgrids, subgrid_size, nr_channels, nr_stations, uvw,
+                 wavenumbers, visibilities, spheroidal, aterms, metadata,
+                 subgrids, validate)
     _check(lib.idg_degridder_launch(
         nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
         nr_channels, nr_stations, _dev_ptr(uvw, "uvw", f32),
@@ -238,6 +285,16 @@ def degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
 # reference).  gridding:   gridder -> subgrid_fft(+1) -> adder
 #              degridding: splitter -> subgrid_fft(-1, 1/S^2) -> degridder
 # ---------------------------------------------------------------------------
+def _pipe_extents(ns, grid_size, S, nr_w_layers, metadata, subgrids, grid):
+    if subgrids.dim() != 5 or tuple(subgrids.shape[1:]) != (4, S, S, 2):
+        raise ValueError("subgrids must be [NS][4][S][S][2] float32")
+    if metadata.numel() * metadata.element_size() != ns * 36:
+        raise ValueError(f"metadata must hold {ns} x 36-byte records")
+    if grid.numel() != nr_w_layers * 4 * grid_size * grid_size * 2:
+        raise ValueError(f"grid must be [{nr_w_layers}][4][{grid_size}]"
+                         f"[{grid_size}][2] float32")
+
+
 def subgrid_fft_launch(subgrids, sign, scale=1.0, stream=None):
     """In-place 2-D DFT of every [S][S] correlation plane of a float32
     [NS, 4, S, S, 2] tensor: out = scale * sum in * exp(sign 2 pi i ...)."""
@@ -252,9 +309,12 @@ def subgrid_fft_launch(subgrids, sign, scale=1.0, stream=None):
 def adder_launch(grid_size, metadata, subgrids, grid, nr_w_layers=1,
                  stream=None):
     """grid [W, 4, G, G, 2] float32 += the FFT'd subgrids placed at their
-    metadata coordinates (float atomics)."""
+    metadata coordinates.  A deterministic gather: each 16x16 grid tile adds
+    the subgrids overlapping it in ascending subgrid order (no atomics on
+    the grid)."""
     import torch
     ns, S = subgrids.shape[0], subgrids.shape[2]
+    _pipe_extents(ns, grid_size, S, nr_w_layers, metadata, subgrids, grid)
     _check(lib.idg_adder_launch(
         ns, grid_size, S, nr_w_layers, _dev_ptr(metadata, "metadata"),
         _dev_ptr(subgrids, "subgrids", torch.float32),
@@ -268,6 +328,7 @@ def splitter_launch(grid_size, metadata, grid, subgrids, nr_w_layers=1,
     of adder_launch's placement)."""
     import torch
     ns, S = subgrids.shape[0], subgrids.shape[2]
+    _pipe_extents(ns, grid_size, S, nr_w_layers, metadata, subgrids, grid)
     _check(lib.idg_splitter_launch(
         ns, grid_size, S, nr_w_layers, _dev_ptr(metadata, "metadata"),
         _dev_ptr(grid, "grid", torch.float32),

@@ -53,6 +53,12 @@ def backend_name():
     return "RCCL over xGMI" if b == "nccl" else b
 
 
+def collectives_on_device():
+    """True when collectives take device tensors (RCCL); gloo takes host
+    tensors for gathers."""
+    return torch_dist.is_initialized() and torch_dist.get_backend() == "nccl"
+
+
 def _device():
     if torch_dist.is_initialized() and \
             torch_dist.get_backend() == "nccl":

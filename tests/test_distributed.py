@@ -138,3 +138,97 @@ def test_gloo_world2_grid_reduce_equals_single_process(tmp_path, oracle_lib):
     ref = pl.adder(np.zeros((1, 4, G, G), complex), a["metadata"],
                    pl.subgrid_fft(pl.to_complex(sg), +1))
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+# ---------------------------------------------------------------------------
+# bench.py's own sharded path (BASELINE configs[3]) at world size 2
+# ---------------------------------------------------------------------------
+SMALL = dict(nr_stations=5, nr_timeslots=3, nr_timesteps=8, nr_channels=3,
+             grid_size=256, subgrid_size=16)
+
+
+def _bench_worker(rank, world, port, out_dir, mode):
+    """One rank of bench.py's sharded run with the oracle standing in for the
+    HIP kernels: bench.make_batch -> bench.shard_batch (this rank's
+    subgrids, rebased metadata, only the rows they read) -> grid + degrid
+    -> subgrid FFT + adder onto a partial grid -> dist.reduce_grid ->
+    bench.dump_outputs (gather in rank order, write on rank 0)."""
+    import sys
+    for p in (PKG, ORACLE, os.path.dirname(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import bench
+    import idg_amd
+    from idg_amd import dist
+    import oracle as orc
+    import pipeline_oracle as pl
+    r, _, w_ = dist.init(backend="gloo")
+    w = dict(SMALL)
+    a = bench.make_batch(w, nthreads=1)
+    part = bench.shard_batch(a, r, w_, mode)
+    n = part["s1"] - part["s0"]
+    S, C, G = w["subgrid_size"], w["nr_channels"], w["grid_size"]
+    p = (n, G, S, idg_amd.IMAGE_SIZE, 0.0, C, w["nr_stations"])
+    o = orc.Oracle()
+    sg = np.zeros((n, 4, S, S, 2), np.float32)
+    o.gridder(*p, part["uvw"], part["wavenumbers"], part["visibilities"],
+              part["spheroidal"], part["aterms"], part["metadata"], sg)
+    vis = np.zeros_like(part["visibilities"])
+    o.degridder(*p, part["uvw"], part["wavenumbers"], vis,
+                part["spheroidal"], part["aterms"], part["metadata"],
+                part["subgrids"])
+    grid = pl.adder(np.zeros((1, 4, G, G), complex), part["metadata"],
+                    pl.subgrid_fft(pl.to_complex(sg), +1))
+    grid = torch.from_numpy(np.ascontiguousarray(pl.to_pairs(grid)))
+    dist.reduce_grid(grid)
+    bench.dump_outputs(out_dir, a, part,
+                       (torch.from_numpy(sg), torch.from_numpy(vis)), grid,
+                       r, w_, mode, dist)
+    dist.finalize()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_gloo_world2_bench_sharded_path_equals_single_rank(tmp_path, mode):
+    """bench.py --gpus 2: the ranks' gathered subgrids and degridded
+    visibilities equal one rank's bit for bit (disjoint shards, the same
+    per-subgrid arithmetic), and the all-reduced grid equals one rank's grid
+    up to float summation order (two partial sums instead of one running
+    sum)."""
+    import pipeline_oracle as pl
+    outs = {}
+    for world in (1, 2):
+        d = str(tmp_path / f"w{world}")
+        mp.start_processes(_bench_worker, args=(world, _free_port(), d, mode),
+                           nprocs=world, join=True, start_method="spawn")
+        outs[world] = {k: np.load(os.path.join(d, k + ".npy"))
+                       for k in ("subgrids", "visibilities", "grid")}
+    one, two = outs[1], outs[2]
+    ns = SMALL["nr_stations"] * (SMALL["nr_stations"] - 1) // 2 * \
+        SMALL["nr_timeslots"]
+    assert one["subgrids"].shape[0] == ns == two["subgrids"].shape[0]
+    assert np.array_equal(one["subgrids"], two["subgrids"])
+    assert np.array_equal(one["visibilities"], two["visibilities"])
+    g1, g2 = pl.to_complex(one["grid"]), pl.to_complex(two["grid"])
+    scale = 2.0 if mode == "replicated" else 1.0  # every rank adds it all
+    assert np.abs(g2 - scale * g1).max() <= 1e-6 * np.abs(g1).max()
+
+
+def test_bench_shard_batch_uploads_only_its_rows():
+    import bench
+    a = bench.make_batch(dict(SMALL), nthreads=1)
+    T, C = SMALL["nr_timesteps"], SMALL["nr_channels"]
+    parts = [bench.shard_batch(a, r, 3) for r in range(3)]
+    assert [p["s1"] - p["s0"] for p in parts] == bench.shard_counts(a, 3)
+    assert sum(p["s1"] - p["s0"] for p in parts) == a["metadata"].size
+    for p in parts:
+        n = p["s1"] - p["s0"]
+        assert p["visibilities"].shape == (n * T, C, 4, 2)
+        assert p["uvw"].shape == (n * T, 3)
+        assert p["metadata"]["time_offset"][0] == 0
+        assert np.array_equal(
+            p["visibilities"].reshape(n, T, C, 4, 2),
+            a["visibilities"][p["s0"]:p["s1"]])
