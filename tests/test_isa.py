@@ -1,0 +1,105 @@
+"""Static checks of the shipped gfx950 kernels' ISA (CPU only: hipcc
+cross-compiles the listing with the library's own flags, `make isa`).
+
+* Wait states around the inline-asm f16 splits that feed the MFMAs
+  (tests/probes/hazard_check.py): every v_mfma SrcA/SrcB
+  written by a VALU has >= 2 wait states before it, every VALU read of a
+  v_sin/v_cos result >= 1, on every control-flow path.
+* Register spills stay out of the MFMA loops: no scratch access inside any
+  basic block that issues an MFMA (DESIGN.md §4.1-4.2 document the few
+  cold spills of the prologue/epilogue).
+"""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from conftest import PKG, REPO
+
+sys.path.insert(0, os.path.join(REPO, "tests", "probes"))
+import hazard_check as hc  # noqa: E402
+
+ISA = os.path.join(PKG, "build", "isa")
+
+
+@pytest.fixture(scope="module")
+def listings():
+    subprocess.run(["make", "-C", PKG, "isa"], check=True,
+                   capture_output=True, timeout=600)
+    return {k: os.path.join(ISA, f"{k}_mi355x.s")
+            for k in ("gridder", "degridder")}
+
+
+SYNTH = """
+_Zkernel:
+\tv_cvt_pk_f16_f32 v10, v1, v2
+\t{pad}
+\tv_mfma_f32_16x16x32_f16 v[0:3], v[10:13], v[20:23], v[0:3]
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+@pytest.mark.parametrize("pad,bad", [("s_nop 1", False), ("s_nop 0", True),
+                                     ("v_add_f32 v30, v31, v32", True),
+                                     ("s_nop 0\n\tv_add_f32 v30, v31, v32",
+                                      False)])
+def test_checker_counts_valu_to_mfma_wait_states(pad, bad):
+    f = hc.parse_functions(SYNTH.format(pad=pad))["_Zkernel"]
+    assert bool(hc.check_function(f)) == bad
+
+
+def test_checker_follows_branches_into_a_loop_head():
+    # the producer sits at the end of the loop body, the MFMA at its head:
+    # only the back edge connects them
+    src = """
+_Zk:
+\ts_nop 4
+.LBB0_1:
+\tv_mfma_f32_16x16x32_f16 v[0:3], v[10:13], v[20:23], v[0:3]
+\ts_nop 7
+\tv_cvt_pk_f16_f32 v11, v1, v2
+\ts_cbranch_scc1 .LBB0_1
+\ts_endpgm
+.Lfunc_end0:
+"""
+    v = hc.check_function(hc.parse_functions(src)["_Zk"])
+    assert [k for k, *_ in v] == ["valu->mfma_src"]
+
+
+def test_checker_trans_forwarding():
+    src = """
+_Zk:
+\tv_sin_f32_e32 v5, v4
+\tv_fma_mixlo_f16 v7, v6, -1.0, v5 op_sel_hi:[1,0,0]
+\ts_endpgm
+.Lfunc_end0:
+"""
+    v = hc.check_function(hc.parse_functions(src)["_Zk"])
+    assert [k for k, *_ in v] == ["trans->valu"]
+
+
+@pytest.mark.parametrize("kernel", ["gridder", "degridder"])
+def test_shipped_kernels_have_no_operand_hazards(listings, kernel):
+    res = hc.check_file(listings[kernel])
+    mfma_kernels = {n: r for n, r in res.items() if r["mfma"]}
+    assert mfma_kernels, "no MFMA kernel found in the listing"
+    bad = {n[:60]: r["violations"][:3] for n, r in res.items()
+           if r["violations"]}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("kernel", ["gridder", "degridder"])
+def test_no_scratch_access_in_mfma_loops(listings, kernel):
+    text = open(listings[kernel]).read()
+    hot = 0
+    for block in re.split(r"\n(?=\.LBB\d+_\d+:|_Z\w+:)", text):
+        if "v_mfma" not in block:
+            continue
+        hot += 1
+        spills = [l.strip() for l in block.split("\n")
+                  if re.match(r"\s*(scratch_|buffer_(load|store)_dword)", l)]
+        assert not spills, spills[:4]
+    assert hot > 0
