@@ -3,7 +3,7 @@
 // Replaces the reference's app/HIP/kernels/degridder_*.hip.cpp behind the same
 // kernel-TU contract (hip::p_run_degridder, hip::c_run_degridder; harness
 // declarations tests/degridder_common.cpp:13-31) and 13-argument kernel ABI
-// (grid = nr_subgrids, block = 256).  It computes
+// (grid = nr_subgrids, block = 256 = 4 wave64).  It computes
 // cpu::kernel_degridder_reference
 // (app/CPU/kernels/degridder_reference.cpp:6-129):
 //
@@ -11,20 +11,20 @@
 //   V_p(t,c) = sum_{y,x} P'_p(y,x) * exp(i*phase),
 //   phase    = fl(phase_index(t,y,x) * k_c - phase_offset(y,x))   [one FMA]
 //
-// Design (DESIGN.md §kernels):
-//  * one workgroup per subgrid; a lane owns one (timestep, group of CG
-//    channels) output unit and keeps CG x 4 complex accumulators in VGPRs;
-//  * the workgroup first writes a pixel table into LDS -- P' (8 floats) and
-//    (l, m, n, phase_offset) per pixel, 48 B, 1024-pixel chunks (48 KiB) --
-//    and every lane then walks the pixels in reference order reading the
-//    table with wave-uniform (broadcast) ds_read_b128;
-//  * phase reduction as in the gridder: per (lane, pixel) the first channel's
-//    phase is converted to revolutions with a Dekker-split 1/(2*pi), the
-//    other channels of the group are exact offsets from it;
+// Design (DESIGN.md §4.2):
+//  * one workgroup per subgrid; default (MODE 1): per channel a real f16
+//    two-term-split GEMM timesteps x pixel pairs x correlation components
+//    on v_mfma_f32_16x16x32_f16 (degrid_mfma below); B (the A-termed,
+//    tapered pixels) is built once per subgrid into LDS;
+//  * the fp32 phase is formed exactly as the reference rounds it and reduced
+//    as fma(phase, 1/2pi_hi, -m) with an integer m per (timestep, pixel,
+//    16-channel block); the tail of 1/2pi_hi is applied to the pixels
+//    (device.hpp: kPhaseTail, phase_tail);
 //  * mirror pixels (even S, w = 0, w_offset = 0): phase(S-1-y, S-1-x) =
-//    -phase(y, x) exactly, so each sin/cos pair serves a pixel pair; the
-//    table then holds pairs (P'(base), P'(mirror), geometry(base));
-//  * 16 v_fma_f32 per (pixel, t, c) complex 4-correlation MAC.
+//    -phase(y, x) exactly, so each sin/cos pair serves a pixel pair;
+//  * IDG_DEGRIDDER_IMPL=valu (MODE 0): the all-VALU kernel, a lane per
+//    (timestep, channel group) unit, 16 v_fma_f32 per (pixel, t, c), phase
+//    anchored per channel group with a Dekker-split 1/(2*pi) (A/B reference).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -96,6 +96,14 @@ __device__ __forceinline__ void pixel_entry(
   geo = make_float4(l, m, n, poff);
 }
 
+// A pixel entry's 4 correlations (pa = xx|xy, pb = yx|yy) times (c, s).
+__device__ __forceinline__ void rotate_entry(float4 &pa, float4 &pb, float c,
+                                             float s) {
+  float v[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+  rotate4(v, c, s);
+  pa = make_float4(v[0], v[1], v[2], v[3]);
+  pb = make_float4(v[4], v[5], v[6], v[7]);
+}
 
 // ---------------------------------------------------------------------------
 // MFMA mirror path (even S, w = 0 for every timestep, w_offset = 0).
@@ -115,7 +123,7 @@ __device__ __forceinline__ void pixel_entry(
 // (x = Bc pair, y = Bs pair) per lane per K-step of 8 pairs -- and the pair
 // geometry are built ONCE per chunk of KP pairs (the whole subgrid when
 // npix/2 <= KP) and reused by every timestep block and channel tile.
-// Per phasor: 1.5 packed phase instructions, v_sin + v_cos, 3 split
+// Per phasor: 1 packed phase instruction, v_sin + v_cos, 3 split
 // instructions, half an MFMA.
 // ---------------------------------------------------------------------------
 template <int KP>
@@ -128,36 +136,31 @@ struct DegridMfmaLds {
 };
 
 // Revolutions of the phases of one pixel at the channel pair kp = (k_j,
-// k_j+1):  fma(fma(p, k, o) - A, 1/2pi, R)  with p, o, A, R taken from half H
-// of their (pixel 0, pixel 1) VGPR pairs and broadcast to both lanes by
+// k_j+1):  fma(fma(p, k, o), 1/2pi_hi, -m)  with p, o and -m taken from half
+// H of their (pixel 0, pixel 1) VGPR pairs and broadcast to both lanes by
 // op_sel, so no operand is duplicated into a register pair (hipcc otherwise
 // materialises the broadcasts or splits the packed FMA into two).  The
-// constant is the inline 1/(2 pi) = kInv2PiHi.  A dependent packed-f32 VALU
-// pair gets one wait state (s_nop 0), as hipcc pads its own; the output is
-// read by compiler code, which pads after the asm itself.
+// constant is the inline 1/(2 pi) = kInv2PiHi; m is the integer revolution
+// count of the anchor block (device.hpp: kPhaseTail).  A dependent
+// packed-f32 VALU pair gets one wait state (s_nop 0), as hipcc pads its own;
+// the output is read by compiler code, which pads after the asm itself.
 template <int H>
 __device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
-                                                   floatx2 o, floatx2 A,
-                                                   floatx2 R) {
+                                                   floatx2 o, floatx2 nm) {
   floatx2 r;
   if constexpr (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]\n\t"
         "s_nop 0\n\t"
-        "v_pk_add_f32 %0, %0, %4 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "s_nop 0\n\t"
-        "v_pk_fma_f32 %0, %0, 0.15915494, %5 op_sel_hi:[1,0,0]"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel_hi:[1,0,0]"
         : "=&v"(r)
-        : "v"(p), "s"(kp), "v"(o), "v"(A), "v"(R));
+        : "v"(p), "s"(kp), "v"(o), "v"(nm));
   else
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,1,1]\n\t"
         "s_nop 0\n\t"
-        "v_pk_add_f32 %0, %0, %4 op_sel:[0,1] op_sel_hi:[1,1] "
-        "neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "s_nop 0\n\t"
-        "v_pk_fma_f32 %0, %0, 0.15915494, %5 op_sel:[0,0,1] "
+        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel:[0,0,1] "
         "op_sel_hi:[1,0,1]"
         : "=&v"(r)
-        : "v"(p), "s"(kp), "v"(o), "v"(A), "v"(R));
+        : "v"(p), "s"(kp), "v"(o), "v"(nm));
   return r;
 }
 static_assert(kInv2PiHi == 0.15915494f, "phase_rev_bcast's inline constant");
@@ -220,10 +223,17 @@ __device__ __forceinline__ void degrid_mfma(
       if (b < half) {
         pixel_entry(b, S, npix, image_size, g, nr_stations, spheroidal,
                     aterms, sg, k.pa[h], k.pb[h], k.geo[h]);
+        // the phase tail of the reduction (device.hpp: kPhaseTail): the
+        // pixel times exp(-i phase_offset eps), its mirror (phase_offset
+        // exactly negated) times exp(+i phase_offset eps)
+        float tc, ts;
+        phase_tail(k.geo[h].w, &tc, &ts);
+        rotate_entry(k.pa[h], k.pb[h], tc, -ts);
         if constexpr (MIRROR) {
           float4 mgeo;
           pixel_entry(npix - 1 - b, S, npix, image_size, g, nr_stations,
                       spheroidal, aterms, sg, k.ma[h], k.mb[h], mgeo);
+          rotate_entry(k.ma[h], k.mb[h], tc, ts);
         }
       }
     }
@@ -347,17 +357,11 @@ __device__ __forceinline__ void degrid_mfma(
           const floatx2 npoff = {-go.x, -go.y};
 #pragma unroll
           for (int jb = 0; jb < CT; jb += CB) {
-            // anchor: phase at the block's first channel, in revolutions
+            // -m: the whole revolutions of the block's first-channel phase
             const floatx2 A = __builtin_elementwise_fma(
                 pidx, floatx2{kk[jb], kk[jb]}, npoff);
-            const floatx2 ih = {kInv2PiHi, kInv2PiHi};
-            const floatx2 hi = A * ih;
-            floatx2 lo = __builtin_elementwise_fma(A, ih, -hi);
-            lo = __builtin_elementwise_fma(A, floatx2{kInv2PiLo, kInv2PiLo},
-                                           lo);
-            const floatx2 R =
-                (hi - floatx2{__builtin_rintf(hi.x), __builtin_rintf(hi.y)}) +
-                lo;
+            const floatx2 t = A * floatx2{kInv2PiHi, kInv2PiHi};
+            const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
             // Packed over channel pairs (j, j+1) per pixel: the wavenumber
             // pair is one SGPR pair and the pixel's terms are broadcast from
             // their halves of the (pixel 0, pixel 1) pairs by op_sel, so the
@@ -366,8 +370,8 @@ __device__ __forceinline__ void degrid_mfma(
 #pragma unroll
             for (int j = jb; j < jb + CB; j += 2) {
               const floatx2 kp = {kk[j], kk[j + 1]};
-              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, A, R);
-              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, A, R);
+              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, nm);
+              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, nm);
               float s0, c0, s1, c1, s2, c2, s3, c3;
               sincos_rev(rx.x, &s0, &c0);  // channel j,   pixel 0
               sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1

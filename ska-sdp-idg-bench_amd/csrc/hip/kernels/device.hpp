@@ -35,6 +35,36 @@ __device__ __forceinline__ float revolutions(float x) {
   return (hi - __builtin_rintf(hi)) + lo;
 }
 
+// kPhaseTail = 1 - 2*pi*kInv2PiHi: the MFMA kernels reduce a phase x to
+// revolutions as r = fma(x, kInv2PiHi, -m), m an integer (the product is
+// exact inside the FMA, |r| < 1, one rounding), which is x/(2*pi) - m minus
+// x * kPhaseTail/(2*pi).  Splitting x = phase_offset - k * phase_index, the
+// phase_offset part of that tail is a constant per pixel and is restored
+// exactly as one phasor exp(i * phase_offset * kPhaseTail) per pixel
+// (phase_tail below, applied after the gridder's sum or to the degridder's
+// pixels); the k * phase_index part, |k * phase_index * kPhaseTail| <=
+// 1.5e-6 rad at C = 256, is left (measured: tests/debug/phase_reduction_emul.py).
+constexpr float kPhaseTail = 0x1.5a892p-25f;  // 4.034206e-8
+
+// exp(i * phase_offset * kPhaseTail), |angle| <= 1.4e-4: cos = 1 - a^2/2
+// (the a^4 term is below 1e-16), sin = a (the a^3 term below 5e-13).
+__device__ __forceinline__ void phase_tail(float phase_offset, float *c,
+                                           float *s) {
+  const float a = phase_offset * kPhaseTail;
+  *c = fma_(-0.5f * a, a, 1.0f);
+  *s = a;
+}
+
+// The 4 correlations (re, im interleaved) times the phasor (c, s).
+__device__ __forceinline__ void rotate4(float (&v)[8], float c, float s) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float re = v[2 * q], im = v[2 * q + 1];
+    v[2 * q] = fma_(re, c, -(im * s));
+    v[2 * q + 1] = fma_(re, s, im * c);
+  }
+}
+
 // sin / cos of 2*pi*r for r in revolutions.  v_sin_f32 / v_cos_f32 take
 // their argument in revolutions and are exact enough once r is small
 // (measured on MI355X: tests/probes); the range

@@ -3,7 +3,8 @@
 // Replaces the reference's app/HIP/kernels/gridder_*.hip.cpp behind the same
 // kernel-TU contract (hip::p_run_gridder, hip::c_run_gridder; the harness
 // forward-declares them at tests/gridder_common.cpp:13-31) and the same
-// 13-argument kernel ABI / launch shape (grid = nr_subgrids, block = 256,
+// 13-argument kernel ABI / launch shape (grid = nr_subgrids, block = the
+// kernel's own: 512 lanes for the MFMA kernel, 256 for the VALU kernel;
 // reference app/HIP/util.cpp:237-244), so it also runs under the reference's
 // own util.cpp.  It computes cpu::kernel_gridder_reference
 // (app/CPU/kernels/gridder_reference.cpp:6-114):
@@ -13,9 +14,12 @@
 //   subgrid  = sph(y,x) * A1^H P A2
 //
 // Design:
-//  * one workgroup (4 wave64) per subgrid;
+//  * one workgroup per subgrid: 8 wave64 (MFMA kernel), 4 (VALU kernel);
 //  * the fp32 phase is formed exactly as the reference rounds it and reduced
-//    without losing its low bits (device.hpp:revolutions + per-block anchor);
+//    to revolutions without losing its low bits: r = fma(phase, 1/2pi_hi,
+//    -m) with an integer m per (pixel, timestep, channel block), and the
+//    tail phase * (1/2pi - 1/2pi_hi) applied to each pixel as one phasor
+//    exp(i * phase_offset * kPhaseTail) in the epilogue (device.hpp);
 //  * default (MODE 1): the complex MAC runs on the matrix cores as f16
 //    two-term-split GEMMs (v_mfma_f32_16x16x32_f16, grid_mfma below), pixels
 //    x (timestep, channel) x correlation components;
@@ -200,8 +204,8 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 //   [cA_h, cB_h, cA_l, cB_l, cC_h, cD_h, cC_l, cD_l]
 // (split_pair on channel pairs: one v_cvt_pk + two v_fma_mix per pair) and
 // B's rows for it are (bcA, bcB, bcA, bcB, bcC, bcD, bcC, bcD): 4 dwords
-// (x, x, y, y) per lane, stored pre-expanded in LDS.  Per phasor: 1.5 packed
-// phase instructions, v_sin + v_cos, 3 split instructions, half an MFMA.
+// (x, x, y, y) per lane, stored pre-expanded in LDS.  Per phasor: 1 packed
+// phase instruction, v_sin + v_cos, 3 split instructions, half an MFMA.
 // ---------------------------------------------------------------------------
 #ifndef IDG_GRID_KSBUF
 #define IDG_GRID_KSBUF 32
@@ -369,7 +373,7 @@ __device__ __forceinline__ void grid_mfma(
             const idg::UVWCoordinate<float> c = {c4.x, c4.y, c4.z};
             const floatx2 cu = {c.u, c.u}, cv = {c.v, c.v};
             const floatx2 ih = {kInv2PiHi, kInv2PiHi};
-            floatx2 NP[PH], A2[PH], R2[PH];
+            floatx2 NP[PH], NM[PH];
 #pragma unroll
             for (int h = 0; h < PH; ++h) {
               // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
@@ -379,16 +383,12 @@ __device__ __forceinline__ void grid_mfma(
                 pidx = __builtin_elementwise_fma(floatx2{c.w, c.w}, N2[h],
                                                  pidx);
               NP[h] = -pidx;
-              // anchor: phase at the block's first channel, in revolutions
+              // -m: the whole revolutions of the block's first-channel
+              // phase, so every r below stays within ~0.7 revolutions
               const floatx2 a =
                   __builtin_elementwise_fma(NP[h], floatx2{ka, ka}, PG2[h]);
-              const floatx2 hi = a * ih;
-              floatx2 lo = __builtin_elementwise_fma(a, ih, -hi);
-              lo = __builtin_elementwise_fma(
-                  a, floatx2{kInv2PiLo, kInv2PiLo}, lo);
-              const floatx2 rn = {__builtin_rintf(hi.x), __builtin_rintf(hi.y)};
-              A2[h] = a;
-              R2[h] = (hi - rn) + lo;
+              const floatx2 t = a * ih;
+              NM[h] = floatx2{-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
             }
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
@@ -401,25 +401,16 @@ __device__ __forceinline__ void grid_mfma(
               const half8 bfy = pack4(by.x, by.y, by.z, by.w);
 #pragma unroll
               for (int h = 0; h < PH; ++h) {
-                // r[j] = (revolutions of channel 4u+j) for tiles (2h, 2h+1)
+                // r[j] = (revolutions of channel 4u+j) for tiles (2h, 2h+1):
+                // the reference's phase, then phase * 1/2pi_hi - m exactly
+                // rounded once (the product is exact inside the FMA)
                 float snx[4], csx[4], sny[4], csy[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                   const float kj = kb[4 * u + j];
-#if IDG_GRID_SCALAR_PHASE
-                  // unpacked: v_pk_*_f32 beside MFMAs can cost more than
-                  // two scalar ops (A/B knob)
-                  floatx2 r;
-                  r.x = fma_(fma_(NP[h].x, kj, PG2[h].x) - A2[h].x, kInv2PiHi,
-                             R2[h].x);
-                  r.y = fma_(fma_(NP[h].y, kj, PG2[h].y) - A2[h].y, kInv2PiHi,
-                             R2[h].y);
-#else
                   const floatx2 ph =
                       __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
-                  const floatx2 r =
-                      __builtin_elementwise_fma(ph - A2[h], ih, R2[h]);
-#endif
+                  const floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
@@ -473,14 +464,22 @@ __device__ __forceinline__ void grid_mfma(
       const float y[8] = {yh0.x + yl0.x, yh0.y + yl0.y, yh0.z + yl0.z,
                           yh0.w + yl0.w, yh1.x + yl1.x, yh1.y + yl1.y,
                           yh1.z + yl1.z, yh1.w + yl1.w};
+      // the phase tail of the reduction: base pixel * exp(i poff eps),
+      // mirror pixel (phase_offset -poff) * exp(-i poff eps)
+      float l, m, n, poff;
+      pixel_geometry(b, S, image_size, g, l, m, n, poff);
+      float tc, ts;
+      phase_tail(poff, &tc, &ts);
       float ab[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) ab[j] = (x[j] + y[j]) * unscale;
+      rotate4(ab, tc, ts);
       store_pixel(ab, b, S, npix, g, nr_stations, spheroidal, aterms, out);
       if constexpr (MIRROR) {
         float am[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) am[j] = (x[j] - y[j]) * unscale;
+        rotate4(am, tc, -ts);
         store_pixel(am, npix - 1 - b, S, npix, g, nr_stations, spheroidal,
                     aterms, out);
       }
@@ -664,10 +663,13 @@ void c_run_gridder(
     idg::Array4D<idg::Matrix2x2<std::complex<float>>> &aterms,
     idg::Array1D<idg::Metadata> &metadata,
     idg::Array4D<std::complex<float>> &subgrids) {
+  // func = nullptr: c_run_gridder_ selects the MI355X kernel for the
+  // problem (S, C, IDG_GRIDDER_IMPL) and launches it with that kernel's own
+  // block size, so no thread count is passed.
   c_run_gridder_(nr_subgrids, grid_size, subgrid_size, image_size,
                  w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
                  visibilities, spheroidal, aterms, metadata, subgrids, nullptr,
-                 idg_mi355x::kBlock);
+                 0);
 }
 
 }  // namespace hip
