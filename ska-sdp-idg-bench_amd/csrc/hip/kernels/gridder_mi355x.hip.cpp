@@ -175,6 +175,10 @@ __device__ __forceinline__ void store_pixel(
         make_float2(pix[q].re * sph, pix[q].im * sph);
 }
 
+// W_TERMS = false: the caller guarantees w_offset = 0 (mirror subgrids), so
+// phase_offset = fma(0, n, x) = x and n (a divide and a square root) is not
+// formed; n is returned as 0.
+template <bool W_TERMS = true>
 __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
                                                const SubgridSetup &g,
                                                float &l, float &m, float &n,
@@ -182,9 +186,14 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
   const int y = p / S, x = p - (p / S) * S;
   l = idg::compute_l(x, S, image_size);
   m = idg::compute_m(y, S, image_size);
-  n = idg::compute_n(l, m);
   // phase_offset = fma(w_o, n, fma(u_o, l, v_o*m))
-  poff = fma_(g.w_offset, n, fma_(g.u_offset, l, g.v_offset * m));
+  if constexpr (W_TERMS) {
+    n = idg::compute_n(l, m);
+    poff = fma_(g.w_offset, n, fma_(g.u_offset, l, g.v_offset * m));
+  } else {
+    n = 0.0f;
+    poff = fma_(g.u_offset, l, g.v_offset * m);
+  }
 }
 
 
@@ -286,7 +295,7 @@ __device__ __forceinline__ void grid_mfma(
     for (int i = 0; i < PT; ++i) {
       const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
       float l, m, n, pg;
-      pixel_geometry(b, S, image_size, g, l, m, n, pg);
+      pixel_geometry<!MIRROR>(b, S, image_size, g, l, m, n, pg);
       L2[i / 2][i % 2] = l;
       M2[i / 2][i % 2] = m;
       N2[i / 2][i % 2] = n;
@@ -322,17 +331,28 @@ __device__ __forceinline__ void grid_mfma(
           const float *vsubf = reinterpret_cast<const float *>(vsub);
           const int nks = nq * nj;
           const bool full = (q0 + nq) * 4 <= nt && 4 * (j0 + nj) <= C;
-          for (int ks = wave; ks < nks; ks += NW) {
-            const int qq = ks / nj, jj = ks - qq * nj;
+          // K-steps are wave-uniform (scalar loop, qq/jj on the SALU), the
+          // block base pointer too; the lane adds a 32-bit byte offset that
+          // is fixed for the kernel (timestep group grp, column words), so
+          // the loads take the SGPR-base + VGPR-offset form with no 64-bit
+          // address arithmetic per K-step.
+          const int wv = __builtin_amdgcn_readfirstlane(wave);
+          const unsigned off_c = (grp * C * 8 + w_c) * 4u;
+          const unsigned off_s = (grp * C * 8 + w_s) * 4u;
+          int qq = wv / nj, jj = wv - (wv / nj) * nj;
+          for (int ks = wv; ks < nks; ks += NW) {
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
             float bc[4], bs[4];
             if (full) {
-              const float *src = vsubf + (t * C + c0) * 8;
+              const char *blk = reinterpret_cast<const char *>(
+                  vsubf + ((q0 + qq) * 4 * C + c0) * 8);
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
-                bc[u] = src[8 * u + w_c] * scale;
-                bs[u] = src[8 * u + w_s] * sc_s;
+                bc[u] = *reinterpret_cast<const float *>(blk + off_c + 32 * u) *
+                        scale;
+                bs[u] = *reinterpret_cast<const float *>(blk + off_s + 32 * u) *
+                        sc_s;
               }
             } else {
 #pragma unroll
@@ -342,6 +362,11 @@ __device__ __forceinline__ void grid_mfma(
                 bc[u] = ok ? vsubf[it * 8 + w_c] * scale : 0.0f;
                 bs[u] = ok ? vsubf[it * 8 + w_s] * sc_s : 0.0f;
               }
+            }
+            jj += NW;
+            while (jj >= nj) {
+              jj -= nj;
+              ++qq;
             }
             const unsigned xc = split_part(bc[0], bc[1], bpart);
             const unsigned yc = split_part(bc[2], bc[3], bpart);
@@ -467,7 +492,7 @@ __device__ __forceinline__ void grid_mfma(
       // the phase tail of the reduction: base pixel * exp(i poff eps),
       // mirror pixel (phase_offset -poff) * exp(-i poff eps)
       float l, m, n, poff;
-      pixel_geometry(b, S, image_size, g, l, m, n, poff);
+      pixel_geometry<!MIRROR>(b, S, image_size, g, l, m, n, poff);
       float tc, ts;
       phase_tail(poff, &tc, &ts);
       float ab[8];
