@@ -384,7 +384,7 @@ __device__ __forceinline__ void degrid_mfma(
             }
           }
           // one K-step's MFMAs stay in their iteration
-          __builtin_amdgcn_sched_barrier(0);
+          IDG_KSTEP_FENCE();
         }
       }
 

@@ -456,7 +456,7 @@ __device__ __forceinline__ void grid_mfma(
               // loop body, the last tile's accumulators came out corrupted
               // (a few % of subgrids, run-to-run different, only with >1
               // wave per SIMD; DESIGN.md §4.4, tests/debug/diff_detail.py).
-              __builtin_amdgcn_sched_barrier(0);
+              IDG_KSTEP_FENCE();
             }
           }
         }

@@ -13,6 +13,14 @@
 
 #include <hip/hip_runtime.h>
 
+// A scheduling fence after each K-step's MFMAs; the
+// IDG_NO_KSTEP_FENCE build is an A/B timing variant only.
+#ifdef IDG_NO_KSTEP_FENCE
+#define IDG_KSTEP_FENCE() ((void)0)
+#else
+#define IDG_KSTEP_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 namespace idg_mi355x {
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
