@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 1 ? IDG_DEGRID_WAVES : 1)
                             const float2 *__restrict__ subgrids) {
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
-  const int s = blockIdx.x;
+  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);

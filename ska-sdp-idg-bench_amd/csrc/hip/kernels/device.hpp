@@ -95,6 +95,21 @@ __device__ __forceinline__ void sincos_rev(float r, float *s, float *c) {
 #endif
 }
 
+// Subgrid of workgroup `orig` among nwg: blocks are dealt round-robin over
+// the 8 XCDs (blocks b and b + 8 share one L2), so the bijective remap below
+// gives each XCD a contiguous run of subgrids (MI355X_MICROARCH.md, XCD
+// placement; cdna_hip_programming.md T1).  Neighbouring subgrids share
+// stations, so their A-term reads hit the same L2.  A speed choice only:
+// any placement computes the same outputs.
+__device__ __forceinline__ int xcd_subgrid(int orig, int nwg) {
+#ifdef IDG_NO_XCD_REMAP
+  return orig;
+#else
+  const int q = nwg / 8, r = nwg % 8, x = orig % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+#endif
+}
+
 // Per-subgrid constants, evaluated exactly as the reference does
 // (gridder_reference.cpp:15-39): offsets in double, rounded to float.
 struct SubgridSetup {

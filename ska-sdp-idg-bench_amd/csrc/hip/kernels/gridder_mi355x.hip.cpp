@@ -230,8 +230,27 @@ struct MfmaLds {
   // uvw of the fill's timesteps (at most 4 * kKsBuf), float4 each
   static constexpr int kUvwOff =
       kObufFloats > kBbufWords ? kObufFloats : kBbufWords;
-  static constexpr int kWords = kUvwOff + 4 * 4 * kKsBuf + 8;
+  static constexpr int kRedOff = kUvwOff + 4 * 4 * kKsBuf;  // 8 floats
+  static constexpr int kSlotOff = kRedOff + 8;   // 2 fill maxima (bits)
+  static constexpr int kSinkOff = kSlotOff + 2;  // 64 words: prefetch sink
+  static constexpr int kWords = kSinkOff + 64;
 };
+
+// LDS-DMA of 4 bytes per lane from the lane's global address into
+// lds_dst + 4 * lane (lds_dst wave-uniform), as inline asm: the gridder uses
+// it only to pull the next fill's rows into L2 (the LDS words are a sink
+// nobody reads), and hipcc, which cannot see the asm, inserts no wait for
+// it; every __syncthreads() drains it (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void l2_prefetch_dma(const void *src,
+                                                const void *lds_dst) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(
+      reinterpret_cast<size_t>((const __attribute__((address_space(3))) void *)
+                                   lds_dst)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off"
+               :
+               : "v"(src), "s"(m0)
+               : "memory");
+}
 
 template <int S_CT, int PT, int CB, int NW, bool MIRROR>
 __device__ __forceinline__ void grid_mfma(
@@ -250,13 +269,25 @@ __device__ __forceinline__ void grid_mfma(
   const int half = MIRROR ? npix / 2 : npix;
   const int nt = g.nr_timesteps;
   const int nchq = (C + 3) / 4;  // channel quads
+  const int nquads = (nt + 3) / 4;
+  const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
+  const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
+  unsigned *slots = lds + MfmaLds<PT, NW>::kSlotOff;
 
-  // Per-subgrid power-of-two scale keeps every visibility inside f16 range.
+  // A power-of-two scale 2^-e keeps the visibilities inside f16 range.  It
+  // is set by the maximum over the first fill's timesteps (all channels),
+  // and every fill reports its own maximum (an integer LDS max of the
+  // non-negative float bits): a fill whose values would leave the range
+  // (|V| 2^-e >= 2^15), or the first non-zero fill when the scale is not
+  // yet set, is split again with the new scale after the f32 sums so far
+  // are rescaled by the exact power of two.  Each input byte is thus read
+  // once per fill (the first fill's rows twice, back to back, from L2).
   float vmax = 0.0f;
   {
+    if (tid < 2) slots[tid] = 0u;
     const float4 *v4 = reinterpret_cast<const float4 *>(
         visibilities + g.time_offset * C * 4);
-    const int n4 = nt * C * 2;
+    const int n4 = min(4 * quads_per_fill, nt) * C * 2;
     for (int i = tid; i < n4; i += NW * 64) {
       const float4 q = v4[i];
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)),
@@ -264,24 +295,23 @@ __device__ __forceinline__ void grid_mfma(
     }
     for (int off = 32; off > 0; off >>= 1)
       vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT, NW>::kWords - 8);
+    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT, NW>::kRedOff);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < NW; ++w) vmax = fmaxf(vmax, red[w]);
   }
   int e = 0;
-  if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
-  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
+  bool have_scale = vmax > 0.0f && vmax <= 3.0e38f;
+  if (have_scale) frexpf(vmax, &e);
+  float scale = ldexpf(1.0f, -e);
+  int fidx = 0;  // fills so far (parity selects the fill's max slot)
 
   const float2 *__restrict__ vsub = visibilities + g.time_offset * C * 4;
 
   uint4 *bbuf = reinterpret_cast<uint4 *>(lds);  // [ks][64][X, Y]
   float *obuf = reinterpret_cast<float *>(lds);
   float4 *tuvw = reinterpret_cast<float4 *>(lds + MfmaLds<PT, NW>::kUvwOff);
-  const int nquads = (nt + 3) / 4;
-  const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
-  const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
 
   constexpr int kPass = NW * 16 * PT;  // base pixels per pass
   for (int gbase = 0; gbase < half; gbase += kPass) {
@@ -310,13 +340,18 @@ __device__ __forceinline__ void grid_mfma(
 
     for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
       const int nq = min(quads_per_fill, nquads - q0);
-      for (int j0 = 0; j0 < nchq; j0 += cq_per_fill) {
+      for (int j0 = 0; j0 < nchq; j0 += cq_per_fill, ++fidx) {
         const int nj = min(cq_per_fill, nchq - j0);
         // ---- B fragments for nq timestep quads x nj channel quads -> LDS.
         // One wave fills one K-step (lane = group g, column col): items
         // (t = 4q+g, c0..c0+3), two word loads each, scaled, then split to
-        // the column's f16 part.
+        // the column's f16 part.  Redone (rarely) when the fill's maximum
+        // leaves the scale's range.
+        for (;;) {
         __syncthreads();
+        // the other slot was read before this barrier; it is next written
+        // by the following fill, after the barrier that ends this one
+        if (tid == 0) slots[(fidx + 1) & 1] = 0u;
         {
           // this lane's B column: correlation bpol, re (even col) or im
           // (odd col) part, and which f16 part (hi: 0, lo: -1) it holds.
@@ -340,6 +375,7 @@ __device__ __forceinline__ void grid_mfma(
           const unsigned off_c = (grp * C * 8 + w_c) * 4u;
           const unsigned off_s = (grp * C * 8 + w_s) * 4u;
           int qq = wv / nj, jj = wv - (wv / nj) * nj;
+          float lmax = 0.0f;  // max |raw value| this lane loads
           for (int ks = wv; ks < nks; ks += NW) {
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
@@ -349,18 +385,24 @@ __device__ __forceinline__ void grid_mfma(
                   vsubf + ((q0 + qq) * 4 * C + c0) * 8);
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
-                bc[u] = *reinterpret_cast<const float *>(blk + off_c + 32 * u) *
-                        scale;
-                bs[u] = *reinterpret_cast<const float *>(blk + off_s + 32 * u) *
-                        sc_s;
+                const float rc =
+                    *reinterpret_cast<const float *>(blk + off_c + 32 * u);
+                const float rs =
+                    *reinterpret_cast<const float *>(blk + off_s + 32 * u);
+                lmax = fmaxf(lmax, fmaxf(fabsf(rc), fabsf(rs)));
+                bc[u] = rc * scale;
+                bs[u] = rs * sc_s;
               }
             } else {
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
                 const bool ok = t < nt && c0 + u < C;
                 const int it = ok ? t * C + c0 + u : 0;
-                bc[u] = ok ? vsubf[it * 8 + w_c] * scale : 0.0f;
-                bs[u] = ok ? vsubf[it * 8 + w_s] * sc_s : 0.0f;
+                const float rc = ok ? vsubf[it * 8 + w_c] : 0.0f;
+                const float rs = ok ? vsubf[it * 8 + w_s] : 0.0f;
+                lmax = fmaxf(lmax, fmaxf(fabsf(rc), fabsf(rs)));
+                bc[u] = rc * scale;
+                bs[u] = rs * sc_s;
               }
             }
             jj += NW;
@@ -375,6 +417,20 @@ __device__ __forceinline__ void grid_mfma(
             bbuf[(ks * 64 + lane) * 2] = make_uint4(xc, xc, yc, yc);
             bbuf[(ks * 64 + lane) * 2 + 1] = make_uint4(xs, xs, ys, ys);
           }
+          // wave max (rows of 16 by DPP, then the four row maxima), one LDS
+          // atomic per wave (an atomicMax from every lane would be expanded
+          // into a 64-step scalar loop by the atomic optimizer)
+          {
+            unsigned v = __float_as_uint(lmax);
+            v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+            v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+            v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));
+            v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));
+            const unsigned wmax =
+                max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                    max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+            if (lane == 0) atomicMax(&slots[fidx & 1], wmax);
+          }
           // the fill's timesteps' uvw, so the MFMA loop reads LDS, not HBM
           for (int i = tid; i < nq * 4; i += NW * 64) {
             const idg::UVWCoordinate<float> c =
@@ -383,6 +439,51 @@ __device__ __forceinline__ void grid_mfma(
           }
         }
         __syncthreads();
+        // The fill's maximum against the scale (wave-uniform branch).
+        const float fm = __uint_as_float(
+            __builtin_amdgcn_readfirstlane(slots[fidx & 1]));
+        if (!(fm > 0.0f && fm <= 3.0e38f)) break;  // all zero (or non-finite)
+        int em;
+        frexpf(fm, &em);
+        if (have_scale ? em <= e + 15 : em == e) {
+          have_scale = true;
+          break;
+        }
+        // Out of range: rescale the sums so far (zero while the scale was
+        // unset) and split this fill again; the slot keeps the fill's max.
+        if (have_scale) {
+          const float r = ldexpf(1.0f, e - em);
+#pragma unroll
+          for (int i = 0; i < PT; ++i) {
+            accx[i] *= r;
+            accy[i] *= r;
+          }
+        }
+        e = em;
+        scale = ldexpf(1.0f, -e);
+        have_scale = true;
+        }
+        // Pull the next fill's rows into L2 while this fill's MFMA loop
+        // runs (one 4-byte LDS-DMA per 128-byte line, into a sink).
+        {
+          int q0n = q0, j0n = j0 + cq_per_fill;
+          if (j0n >= nchq) {
+            j0n = 0;
+            q0n = q0 + quads_per_fill;
+          }
+          if (q0n < nquads) {
+            const int rows = min(4 * (q0n + quads_per_fill), nt) - 4 * q0n;
+            const int lpr = (min(cq_per_fill, nchq - j0n) * 128 + 127) / 128;
+            const char *vb = reinterpret_cast<const char *>(vsub);
+            for (int ln = tid; ln < rows * lpr; ln += NW * 64) {
+              const int row = ln / lpr, cl = ln - (ln / lpr) * lpr;
+              l2_prefetch_dma(
+                  vb + (static_cast<size_t>(4 * q0n + row) * C + 4 * j0n) * 32 +
+                      cl * 128,
+                  lds + MfmaLds<PT, NW>::kSinkOff);
+            }
+          }
+        }
         // ---- MFMA over the buffered K-steps ----
         // Channel blocks outermost: the block's CB wavenumbers are loaded
         // into SGPRs once per fill, not once per timestep quad.
@@ -463,6 +564,7 @@ __device__ __forceinline__ void grid_mfma(
       }
     }
 
+    const float unscale = ldexpf(1.0f, e);
     // ---- epilogue: X, Y tiles -> LDS [pixel][16]; base = X + Y, mirror =
     // X - Y; hi + lo; A-term; store ----
     __syncthreads();
@@ -538,7 +640,7 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
   constexpr int NB = PPT / 2;
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
-  const int s = blockIdx.x;
+  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);

@@ -169,13 +169,13 @@ def test_w_terms_vs_oracle(idg, oracle_lib, geom):
                                      "zero_then_tiny", "burst_wterm"])
 def test_gridder_fill_scale_paths_vs_oracle(idg, oracle_lib, pattern):
     """The gridder's f16 B-fragment scale is taken from the first fill's
-    timesteps (32 timesteps x 16 channels here; the whole subgrid when those
-    are all zero); a later value beyond f16 range leaves non-finite sums and
-    the pass runs again with the whole subgrid's maximum.  Visibility
-    magnitudes that take every branch: all 1e6, all 1e-6, a 1e6 burst in
-    the last fill only (overflow -> re-run), leading all-zero fills followed
-    by 1e-6 values (whole-subgrid maximum), and the burst on the general
-    (w != 0) path."""
+    timesteps (32 timesteps x 16 channels here); every fill reports its own
+    maximum, and a fill whose scaled values would reach 2^15 (or the first
+    non-zero fill while no scale is set) is split again after the f32 sums
+    so far are rescaled by the exact power of two.  Visibility magnitudes
+    that take every branch: all 1e6, all 1e-6, a 1e6 burst in the last fill
+    only (rescale), leading all-zero fills followed by 1e-6 values (scale
+    set late), and the burst on the general (w != 0) path."""
     st, ts, T, C, G, S = 3, 1, 96, 16, 1024, 32
     a = idg.generate(st, ts, T, C, G, S)
     vis = a["visibilities"]

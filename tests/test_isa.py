@@ -103,3 +103,16 @@ def test_no_scratch_access_in_mfma_loops(listings, kernel):
                   if re.match(r"\s*(scratch_|buffer_(load|store)_dword)", l)]
         assert not spills, spills[:4]
     assert hot > 0
+
+
+def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
+    # The gridder pulls each next fill's rows into L2 with a 4-byte LDS-DMA
+    # issued as inline asm after the fill barrier.  A
+    # compiler vmcnt wait between it and the MFMA loop (e.g. for a spill
+    # reload) would expose its whole latency once per fill.
+    import dma_drain_check as ddc
+    res = ddc.check(open(listings["gridder"]).read())
+    mfma_kernels = [r for r in res if "ELi1ELi4EE" in r[0]]
+    assert mfma_kernels, "no gridder kernel with an LDS-DMA prefetch"
+    for name, total, drained, _ in mfma_kernels:
+        assert total > 0 and drained == 0, (name[:60], total, drained)
