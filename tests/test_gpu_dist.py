@@ -66,3 +66,33 @@ def test_bench_two_ranks_sharded_equals_one_rank(tmp_path):
                           got["two"]["visibilities"])
     g1, g2 = got["one"]["grid"], got["two"]["grid"]
     assert np.abs(g2 - g1).max() <= 1e-6 * np.abs(g1).max()
+
+
+@pytest.mark.timeout(600)
+def test_bench_collectives_over_rccl_single_rank(tmp_path):
+    """The RCCL side of the same path on the box's one device: bench.py runs
+    inside an "nccl" (RCCL) process group of world size 1, so its barrier
+    (device_ids), max/sum over ranks on device tensors, the uv-grid
+    all-reduce and the output gathers all go through RCCL.  Outputs must equal
+    the run without a process group bit for bit (a one-rank all-reduce is the
+    identity).  The 8-GPU run differs only in the world size."""
+    common = ["--gpus", "1", "--steps", "2", "--warmup", "1", "--timeslots",
+              "2", "--no-cpu-baseline"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    plain = _run([sys.executable, "bench.py", "--dump", str(tmp_path / "plain")]
+                 + common, env)
+    code = ("import sys, torch, torch.distributed as d\n"
+            "torch.cuda.set_device(0)\n"
+            f"d.init_process_group('nccl', init_method='tcp://127.0.0.1:{_port()}',"
+            " rank=0, world_size=1, device_id=torch.device('cuda', 0))\n"
+            "assert d.get_backend() == 'nccl'\n"
+            "sys.path.insert(0, '.')\n"
+            "import bench\n"
+            "bench.main(sys.argv[1:])\n")
+    rccl = _run([sys.executable, "-c", code, "--dump", str(tmp_path / "rccl")]
+                + common, env)
+    assert rccl["n_gpus"] == 1 and rccl["value"] > 0
+    for k in ("subgrids", "visibilities", "grid"):
+        a = np.load(tmp_path / "plain" / (k + ".npy"))
+        b = np.load(tmp_path / "rccl" / (k + ".npy"))
+        assert np.array_equal(a, b), k
