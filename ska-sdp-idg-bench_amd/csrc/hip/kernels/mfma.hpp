@@ -40,25 +40,23 @@ __device__ __forceinline__ half2 split_f16(float x) {
 }
 
 // Splits the pair (c, s): *hi = (f16(c), f16(s)), *lo = (f16(c - hi.c),
-// f16(s - hi.s)) in 3 instructions (v_cvt_pk_f16_f32 + v_fma_mix{lo,hi}_f16;
-// the residual c - hi.c is exact in f32 and rounded once to f16).
+// f16(s - hi.s)): v_cvt_pk_f16_f32, the two f32 residuals (exact) by
+// v_fma_mix_f32, one more v_cvt_pk_f16_f32 (the same single rounding as an
+// f16-output v_fma_mix, at full issue rate; split_oct below).
 __device__ __forceinline__ void split_pair(float c, float s, unsigned *hi,
                                            unsigned *lo) {
   floatx2 v = {c, s};
   const f16x2 h = __builtin_convertvector(v, f16x2);
   const unsigned hu = __builtin_bit_cast(unsigned, h);
-  unsigned lu;
-  asm volatile("s_nop 0\n\tv_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]"
-               : "=&v"(lu)
-               : "v"(hu), "v"(c));
-  asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] "
-               "op_sel_hi:[1,0,0]\n\ts_nop 1"
-               : "+v"(lu)
-               : "v"(hu), "v"(s));
+  float rc, rs;
+  asm volatile("s_nop 0\n\tv_fma_mix_f32 %0, %2, -1.0, %3 op_sel_hi:[1,0,0]\n\t"
+               "v_fma_mix_f32 %1, %2, -1.0, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+               : "=&v"(rc), "=&v"(rs)
+               : "v"(hu), "v"(c), "v"(s));
   *hi = hu;
-  *lo = lu;
+  *lo = __builtin_bit_cast(unsigned,
+                           __builtin_convertvector(floatx2{rc, rs}, f16x2));
 }
-
 // Four packed-f16 dwords as the 8-element MFMA operand.
 __device__ __forceinline__ half8 pack4(unsigned a, unsigned b, unsigned c,
                                        unsigned d) {
@@ -70,20 +68,19 @@ __device__ __forceinline__ half8 pack4(unsigned a, unsigned b, unsigned c,
 // One f16 part of each of (a, b), packed: the hi part f16(x) where
 // m = 0, the lo part f16(x - f16(x)) where m = -1 (m is per lane, so lanes
 // holding B's hi columns and lanes holding its lo columns run the same
-// three instructions).
+// instructions): m * f16(x) + x is exact in f32 (v_fma_mix_f32), then one
+// v_cvt_pk_f16_f32 rounds both.
 __device__ __forceinline__ unsigned split_part(float a, float b, float m) {
   floatx2 v = {a, b};
   const unsigned hu =
       __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
-  unsigned r;
-  asm volatile("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]"
-               : "=&v"(r)
-               : "v"(hu), "v"(m), "v"(a));
-  asm volatile("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] "
-               "op_sel_hi:[1,0,0]"
-               : "+v"(r)
-               : "v"(hu), "v"(m), "v"(b));
-  return r;
+  float ra, rb;
+  asm volatile("v_fma_mix_f32 %0, %2, %3, %4 op_sel_hi:[1,0,0]\n\t"
+               "v_fma_mix_f32 %1, %2, %3, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+               : "=&v"(ra), "=&v"(rb)
+               : "v"(hu), "v"(m), "v"(a), "v"(b));
+  return __builtin_bit_cast(unsigned,
+                            __builtin_convertvector(floatx2{ra, rb}, f16x2));
 }
 
 // hi parts (f16(a), f16(b)) packed.
@@ -99,52 +96,45 @@ __device__ __forceinline__ unsigned split_lo(float a, float b) {
   return lo;
 }
 
-// Two split_pair()s in one asm block: returns the MFMA operand dwords
-// (hi(a0, a1), lo(a0, a1), hi(b0, b1), lo(b0, b1)).  hipcc neither models
-// nor pads what is inside an asm string and adds only one wait state after
-// it, so the string carries its own pads: `s_nop 0` first (the inputs are
-// usually fresh v_sin/v_cos results: trans -> VALU forwarding needs 1 state)
-// and `s_nop 1` last (VALU write -> MFMA SrcA read needs 2 states; the
-// outputs are the next MFMA's A operand).
-__device__ __forceinline__ half8 split_quad(float a0, float a1, float b0,
-                                            float b1) {
-  unsigned h0, l0, h1, l1;
-  asm("s_nop 0\n\t"
-      "v_cvt_pk_f16_f32 %0, %4, %5\n\t"
-      "v_cvt_pk_f16_f32 %2, %6, %7\n\t"
-      "v_fma_mixlo_f16 %1, %0, -1.0, %4 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %3, %2, -1.0, %6 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %1, %0, -1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %3, %2, -1.0, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "s_nop 1"
-      : "=&v"(h0), "=&v"(l0), "=&v"(h1), "=&v"(l1)
-      : "v"(a0), "v"(a1), "v"(b0), "v"(b1));
-  return pack4(h0, l0, h1, l1);
-}
-
-// Two split_quad()s in one asm block (one pair of pads for both operands):
-// *A = split of (a0, a1, a2, a3), *B = split of (b0, b1, b2, b3).
+// Two operands' splits in one asm block (one pair of pads for both):
+// *A = (hi(a0, a1), lo(a0, a1), hi(a2, a3), lo(a2, a3)), *B likewise for b.
+// The lo parts are formed as f32 residuals r = x - f32(hi) with
+// v_fma_mix_f32 (exact: hi is x rounded to 11 bits) and packed to f16 with
+// one v_cvt_pk_f16_f32 per pair, i.e. f16(x - hi) with the same single
+// rounding as a v_fma_mix{lo,hi}_f16: bit for bit the same operand, but the
+// f16-output mix issues at half rate on gfx950 (8.5 vs 4.5 cycles,
+// tests/probes/instr_rates_probe.hip), so 8 mix_f32 + 4 cvt_pk cost 13
+// cycles less per call than 8 mixlo/hi (split_rates_probe.hip).
+// Pads: `s_nop 0` first (the inputs are usually fresh v_sin/v_cos results:
+// trans -> VALU forwarding needs 1 state) and `s_nop 1` last (VALU write ->
+// MFMA SrcA read needs 2 states; the outputs are the next MFMAs' A operands).
 __device__ __forceinline__ void split_oct(float a0, float a1, float a2,
                                           float a3, float b0, float b1,
                                           float b2, float b3, half8 *A,
                                           half8 *B) {
   unsigned h0, l0, h1, l1, h2, l2, h3, l3;
+  float r0, r1, r2, r3, r4, r5, r6, r7;
   asm("s_nop 0\n\t"
-      "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
-      "v_cvt_pk_f16_f32 %2, %10, %11\n\t"
-      "v_cvt_pk_f16_f32 %4, %12, %13\n\t"
-      "v_cvt_pk_f16_f32 %6, %14, %15\n\t"
-      "v_fma_mixlo_f16 %1, %0, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %3, %2, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %5, %4, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixlo_f16 %7, %6, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %1, %0, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %3, %2, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %5, %4, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %7, %6, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_cvt_pk_f16_f32 %0, %16, %17\n\t"
+      "v_cvt_pk_f16_f32 %2, %18, %19\n\t"
+      "v_cvt_pk_f16_f32 %4, %20, %21\n\t"
+      "v_cvt_pk_f16_f32 %6, %22, %23\n\t"
+      "v_fma_mix_f32 %8, %0, -1.0, %16 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %9, %0, -1.0, %17 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %10, %2, -1.0, %18 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %11, %2, -1.0, %19 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %12, %4, -1.0, %20 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %13, %4, -1.0, %21 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %14, %6, -1.0, %22 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %15, %6, -1.0, %23 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_cvt_pk_f16_f32 %1, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %3, %10, %11\n\t"
+      "v_cvt_pk_f16_f32 %5, %12, %13\n\t"
+      "v_cvt_pk_f16_f32 %7, %14, %15\n\t"
       "s_nop 1"
       : "=&v"(h0), "=&v"(l0), "=&v"(h1), "=&v"(l1), "=&v"(h2), "=&v"(l2),
-        "=&v"(h3), "=&v"(l3)
+        "=&v"(h3), "=&v"(l3), "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3),
+        "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
       : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2),
         "v"(b3));
   *A = pack4(h0, l0, h1, l1);
