@@ -46,9 +46,13 @@ CLOCK_HZ = 2.4e9            # MI355X_MICROARCH.md: max engine clock
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector = FP32 matrix
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA, dense
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Issue cost per wave64 instruction on one SIMD, in cycles at 2.4 GHz
-# (tests/probes/rates_probe.hip, profiles/r01/rates_probe.txt)
-ISSUE_CYC = {"trans": 9.65, "mfma_f16": 8.0, "other": 4.47}
+# Issue cost per wave64 instruction on one SIMD, in cycles at 2.4 GHz, the
+# lower end of the isolated-probe costs (profiles/r02/rates/): v_sin/v_cos
+# 8.35 (instr_rates_probe.hip), "other" = the VOP3/VOP3P class that makes up
+# 97% of the MFMA loops' remaining VALU (v_cvt_pk_f16_f32 4.5, v_fma_mix_f32
+# 4.46, v_pk_fma_f32 4.8), f16 MFMA 4.7 beside the split that feeds it
+# (split_rates_probe.hip: split + 2 dependent MFMAs - split alone, per MFMA).
+ISSUE_CYC = {"trans": 8.35, "mfma_f16": 4.7, "other": 4.46}
 MFMA_F16_FLOP = 16 * 16 * 32 * 2  # v_mfma_f32_16x16x32_f16
 NR_SIMDS = 1024
 
@@ -339,12 +343,12 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled):
     v_sin + v_cos, the two-term f16 split of the MFMA operand and half an
     f16 MFMA, all issued by the same SIMD.  The ceiling is the time the
     kernel's own instruction stream needs at full issue rate:
-        t_issue = (trans x 9.65 + mfma_f16 x 8 + other VALU x 4.47) cycles
+        t_issue = (trans x 8.35 + mfma_f16 x 4.7 + other VALU x 4.46) cycles
                   / 1024 SIMDs / 2.4 GHz
     from the per-launch wave-instruction counts of the committed SQ profile
     (profiles/traffic.json -> issue_bound; scaled by subgrids when this
     launch grids a shard) and the measured issue costs
-    (tests/probes/rates_probe.hip).  achieved = the reference work model's
+    (tests/probes/instr_rates_probe.hip).  achieved = the reference work model's
     FLOPs (app/common/common.cpp:100-129) / measured time; peak = the same
     FLOPs / t_issue; frac = t_issue / t <= 1.  Beside it: executed f16 MFMA
     FLOP/s against the dense f16 peak (mfma), and the work model against the

@@ -31,6 +31,12 @@
 #define PERM(i) "v_perm_b32 %" #i ", %8, %9, %" #i "\n"
 #define MADMIX(i) "v_fma_mixlo_f16 %" #i ", %8, %9, %" #i " op_sel_hi:[0,0,1]\n"
 #define CVTPKRTZ(i) "v_cvt_pkrtz_f16_f32 %" #i ", %8, %9\n"
+#define SIN(i) "v_sin_f32 %" #i ", %" #i "\n"
+#define COS(i) "v_cos_f32 %" #i ", %" #i "\n"
+#define RNDNE(i) "v_rndne_f32 %" #i ", %" #i "\n"
+#define PKMUL(i) "v_pk_mul_f32 %" #i ", %8, %9\n"
+#define MOV(i) "v_mov_b32 %" #i ", %8\n"
+#define CVTPK_DEP(i) "v_cvt_pk_f16_f32 %" #i ", %" #i ", %9\n"
 
 template <int K>
 __global__ void __launch_bounds__(256) rate(float *out, int iters) {
@@ -57,6 +63,11 @@ __global__ void __launch_bounds__(256) rate(float *out, int iters) {
     if (K == 11) R8(PERM);
     if (K == 12) R8(MADMIX);
     if (K == 13) R8(CVTPKRTZ);
+    if (K == 14) R8(SIN);
+    if (K == 15) R8(COS);
+    if (K == 16) R8(RNDNE);
+    if (K == 17) R8P(PKMUL);
+    if (K == 18) R8(MOV);
   }
   float r = 0;
   for (int i = 0; i < 8; ++i) r += __uint_as_float(h[i]) + (float)d[i];
@@ -97,6 +108,11 @@ int main() {
   run<9>("v_pk_fma_f32", out);
   run<10>("v_pk_fma_f16", out);
   run<11>("v_perm_b32", out);
+  run<14>("v_sin_f32", out);
+  run<15>("v_cos_f32", out);
+  run<16>("v_rndne_f32", out);
+  run<17>("v_pk_mul_f32", out);
+  run<18>("v_mov_b32", out);
   (void)hipDeviceSynchronize();
   return 0;
 }

@@ -97,6 +97,11 @@ __global__ void __launch_bounds__(512, 4)
       accy[2 * h + 1] = mfma16(as, bfy, accy[2 * h + 1]);
     }
     IDG_KSTEP_FENCE();
+    // the anchors change per timestep quad in the kernel: keep the phases
+    // loop-variant here too (one v_pk_add per K-step), or the compiler
+    // hoists v_sin/v_cos out of the loop
+    NM[0] = NM[0] + floatx2{1.0f, 1.0f};
+    NM[1] = NM[1] - floatx2{1.0f, 1.0f};
   }
   float r = 0;
   for (int i = 0; i < 4; ++i)

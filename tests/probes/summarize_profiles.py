@@ -11,8 +11,8 @@ Per kernel (the MFMA gridder/degridder of the workload):
   * HBM bytes per launch: FETCH_SIZE x 2 + WRITE_SIZE (KiB), the gfx950
     correction of MI355X_MICROARCH.md (vector loads tallied at 64 B per
     128-B request), calibrated in profiles/r01/traffic_calibration.md;
-  * VALU-issue utilisation: (trans x 9.65 + f16 MFMA x 8 + other VALU x 4.47
-    cycles, tests/probes/rates_probe.hip) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8
+  * VALU-issue utilisation: (trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46
+    cycles, tests/probes/instr_rates_probe.hip) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8
     XCDs).
 """
 import argparse
@@ -28,7 +28,7 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(
     __file__))))
 ROCPD2CSV = "/opt/rocm/bin/rocpd2csv"
-CYC_TRANS, CYC_MFMA_F16, CYC_VALU = 9.65, 8.0, 4.47
+CYC_TRANS, CYC_MFMA_F16, CYC_VALU = 8.35, 4.7, 4.46
 N_SIMD, N_XCD = 1024, 8
 
 
@@ -152,8 +152,8 @@ def main():
             issue = {
                 "resource": "VALU issue per SIMD",
                 "utilization": round(cyc / per_simd, 3),
-                "model": ("(trans x 9.65 + f16 MFMA x 8 + other VALU x 4.47 "
-                          "cycles, tests/probes/rates_probe.hip) / "
+                "model": ("(trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46 "
+                          "cycles, tests/probes/instr_rates_probe.hip) / "
                           "(GRBM_GUI_ACTIVE / 8 XCDs), summed over 1024 SIMDs"),
                 "insts_valu": c["SQ_INSTS_VALU"],
                 "insts_trans": c["SQ_INSTS_VALU_TRANS_F32"],
