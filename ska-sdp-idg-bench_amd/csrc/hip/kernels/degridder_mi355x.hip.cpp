@@ -389,6 +389,36 @@ __device__ __forceinline__ void degrid_mfma(
       }
 
       // D rows = timesteps wave*16 + grp*4 + r, col = component (hi | lo).
+      // hi + lo: row_ror:8 adds lane col+8 to lane col (and col to col+8),
+      // so both half-rows hold the component sums; lanes col < 8 take
+      // channel j's, lanes col >= 8 channel j+1's, and each 16-lane group
+      // writes the two adjacent 32-byte visibilities (t, j), (t, j+1) as one
+      // contiguous 64-byte store -- no LDS shuffle, no inactive lanes.
+      const bool full_tc = t0 + 64 <= nt && cg0 + CT <= C;
+      if (full_tc) {
+        float *vrow = reinterpret_cast<float *>(visibilities) +
+                      (static_cast<size_t>(g.time_offset + t0 + wave * 16 +
+                                           grp * 4) * C + cg0) * 8 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float *dst = vrow + static_cast<size_t>(r) * C * 8;
+#pragma unroll
+          for (int j = 0; j < CT; j += 2) {
+            const float v0 = acc[j][r], v1 = acc[j + 1][r];
+            const float s0 = v0 + __builtin_bit_cast(float,
+                __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v0),
+                                            0x128, 0xF, 0xF, false));
+            const float s1 = v1 + __builtin_bit_cast(float,
+                __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v1),
+                                            0x128, 0xF, 0xF, false));
+            const float out = (col < 8 ? s0 : s1) * unscale;
+            if (pc0 == 0)
+              dst[8 * j] = out;
+            else
+              dst[8 * j] += out;
+          }
+        }
+      } else {
 #pragma unroll
       for (int j = 0; j < CT; ++j) {
         const int ch = cg0 + j;
@@ -404,6 +434,7 @@ __device__ __forceinline__ void degrid_mfma(
             dst[col] = pc0 == 0 ? out : dst[col] + out;
           }
         }
+      }
       }
     }
   }
