@@ -36,6 +36,9 @@
 #define RNDNE(i) "v_rndne_f32 %" #i ", %" #i "\n"
 #define PKMUL(i) "v_pk_mul_f32 %" #i ", %8, %9\n"
 #define MOV(i) "v_mov_b32 %" #i ", %8\n"
+#define XORL(i) "v_xor_b32 %" #i ", 0x808080, %" #i "\n"
+#define XORV(i) "v_xor_b32 %" #i ", %8, %" #i "\n"
+#define ADDF(i) "v_add_f32 %" #i ", %8, %" #i "\n"
 #define CVTPK_DEP(i) "v_cvt_pk_f16_f32 %" #i ", %" #i ", %9\n"
 
 template <int K>
@@ -68,6 +71,9 @@ __global__ void __launch_bounds__(256) rate(float *out, int iters) {
     if (K == 16) R8(RNDNE);
     if (K == 17) R8P(PKMUL);
     if (K == 18) R8(MOV);
+    if (K == 19) R8(XORL);
+    if (K == 20) R8(XORV);
+    if (K == 21) R8(ADDF);
   }
   float r = 0;
   for (int i = 0; i < 8; ++i) r += __uint_as_float(h[i]) + (float)d[i];
@@ -113,6 +119,9 @@ int main() {
   run<16>("v_rndne_f32", out);
   run<17>("v_pk_mul_f32", out);
   run<18>("v_mov_b32", out);
+  run<19>("v_xor_b32 (32-bit literal)", out);
+  run<20>("v_xor_b32 (VGPR)", out);
+  run<21>("v_add_f32", out);
   (void)hipDeviceSynchronize();
   return 0;
 }
