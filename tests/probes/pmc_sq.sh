@@ -13,7 +13,7 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
            "SQ_INSTS_VALU_MFMA_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || echo "pass $i failed"
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
+    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || { echo "pass $i failed"; exit 1; }
 done
 echo done

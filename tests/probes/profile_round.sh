@@ -9,8 +9,8 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ktrace" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 10 --warmup 3 --no-cpu-baseline > "$out/bench_ktrace.json"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
 echo done

@@ -183,7 +183,7 @@ def main():
     with open(os.path.join(args.out, "pmc_sq_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     with open(os.path.join(args.out, "kernel_stats_summary.txt"), "w") as f:
-        f.write("rocprofv3 --kernel-trace --stats of bench.py (default "
+        f.write(f"rocprofv3 --kernel-trace --stats of bench.py ({args.workload} "
                 "workload); per-launch means over the traced launches\n")
         f.write("\n".join(lines) + "\n")
     with open(args.traffic, "w") as f:
