@@ -39,6 +39,8 @@
 #define XORL(i) "v_xor_b32 %" #i ", 0x808080, %" #i "\n"
 #define XORV(i) "v_xor_b32 %" #i ", %8, %" #i "\n"
 #define ADDF(i) "v_add_f32 %" #i ", %8, %" #i "\n"
+#define DOT2C(i) "v_dot2c_f32_f16 %" #i ", %8, %9\n"
+#define DOT2(i) "v_dot2_f32_f16 %" #i ", %8, %9, %" #i "\n"
 #define CVTPK_DEP(i) "v_cvt_pk_f16_f32 %" #i ", %" #i ", %9\n"
 
 template <int K>
@@ -74,6 +76,8 @@ __global__ void __launch_bounds__(256) rate(float *out, int iters) {
     if (K == 19) R8(XORL);
     if (K == 20) R8(XORV);
     if (K == 21) R8(ADDF);
+    if (K == 22) R8(DOT2C);
+    if (K == 23) R8(DOT2);
   }
   float r = 0;
   for (int i = 0; i < 8; ++i) r += __uint_as_float(h[i]) + (float)d[i];
@@ -122,6 +126,8 @@ int main() {
   run<19>("v_xor_b32 (32-bit literal)", out);
   run<20>("v_xor_b32 (VGPR)", out);
   run<21>("v_add_f32", out);
+  run<22>("v_dot2c_f32_f16 (VOP2)", out);
+  run<23>("v_dot2_f32_f16 (VOP3P)", out);
   (void)hipDeviceSynchronize();
   return 0;
 }
