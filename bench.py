@@ -540,6 +540,21 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
                         f"{dist.backend_name()}"
                         if world > 1 else "single rank: no collective"),
     }
+    # HBM roofline of each step: algorithmic bytes (subgrids read/written
+    # once, the grid once per pass) over the busiest rank's time
+    sub_b = sub_out.numel() * 4
+    grid_b = gridt.numel() * 4
+    algo = {"fft_ms": 2 * sub_b, "adder_ms": sub_b + 2 * grid_b,
+            "splitter_ms": sub_b + grid_b, "ifft_ms": 2 * sub_b}
+    roof = {}
+    for k, nbytes in algo.items():
+        t = out[k] / 1e3
+        if t > 0:
+            gbs = nbytes / t / 1e9
+            roof[k[:-3]] = {"algorithmic_bytes": nbytes,
+                            "achieved_gbs": round(gbs, 1),
+                            "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    out["roofline_hbm"] = roof
     return out, gridt
 
 

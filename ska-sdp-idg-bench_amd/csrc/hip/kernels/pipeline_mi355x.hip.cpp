@@ -49,6 +49,38 @@ __device__ __forceinline__ float2 shift_phasor(int x, int y, int S, float sgn) {
   return unit_phasor((x + y) * (S + 1) - S, 2 * S, sgn);
 }
 
+// (v + S/2) % S for 0 <= v < S, without an integer division (S is a
+// runtime value): the fftshift index of subgrid row/column v.
+__device__ __forceinline__ int half_shift(int v, int S) {
+  const int w = v + S / 2;
+  return w >= S ? w - S : w;
+}
+
+// Stores of the FFT and splitter outputs (0.8 GB at configs[1], consumed by
+// a later kernel): non-temporal, so they do not sit dirty in L2 / MALL and
+// the next kernel does not pay for their write-back (measured: splitter
+// 0.266 -> 0.256 ms and the inverse FFT after it 0.306 -> 0.270 ms).
+#ifndef IDG_PIPE_NT
+#define IDG_PIPE_NT 1
+#endif
+__device__ __forceinline__ void store_stream(float2 *p, float2 v) {
+#if IDG_PIPE_NT
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(f2{v.x, v.y}, reinterpret_cast<f2 *>(p));
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void store_stream(float4 *p, float4 v) {
+#if IDG_PIPE_NT
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w},
+                              reinterpret_cast<f4 *>(p));
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ bool fits(const idg::Metadata &m, int G, int S,
                                      int nr_w_layers) {
   return m.coordinate.x >= 0 && m.coordinate.x + S <= G &&
@@ -240,7 +272,7 @@ __global__ void __launch_bounds__(256)
           const int y = ty0 + i / kAddTile - c.y;
           ok[h][j] = e + h < total && x >= 0 && x < S && y >= 0 && y < S;
           const int src =
-              ok[h][j] ? ((y + S / 2) % S) * S + (x + S / 2) % S : 0;
+              ok[h][j] ? half_shift(y, S) * S + half_shift(x, S) : 0;
           ph[h][j] = !ok[h][j] ? make_float2(0.0f, 0.0f)
                      : tabled  ? table[x + y]
                                : shift_phasor(x, y, S, 1.0f);
@@ -348,24 +380,99 @@ __global__ void __launch_bounds__(256)
                     const float2 *__restrict__ grid,
                     float2 *__restrict__ subgrids, int G, int S,
                     int nr_w_layers) {
-  const int s = blockIdx.x;
+  __shared__ float2 table[kAddMaxTable];
+  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const idg::Metadata m = metadata[s];
   const bool inside = fits(m, G, S, nr_w_layers);
   const int npix = S * S;
   float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const float2 *gz =
       grid + static_cast<size_t>(inside ? m.coordinate.z : 0) * 4 * G * G;
-  for (int i = threadIdx.x; i < npix; i += blockDim.x) {
-    const int y = i / S, x = i - y * S;
-    const int dst = ((y + S / 2) % S) * S + (x + S / 2) % S;
-    const float2 ph = shift_phasor(x, y, S, -1.0f);
+  // the shift phasor depends on x + y only: 2S - 1 values per subgrid
+  const bool tabled = 2 * S - 1 <= kAddMaxTable;
+  if (tabled)
+    for (int k = tid; k < 2 * S - 1; k += nt)
+      table[k] = unit_phasor(k * (S + 1) - S, 2 * S, -1.0f);
+  __syncthreads();
+  // pixel (y, x) of i = tid + nt * j, advanced without integer division
+  const int dy = nt / S, dx = nt - (nt / S) * S;
+  int y = tid / S, x = tid - (tid / S) * S;
+  for (int i = tid; i < npix; i += nt) {
+    const int dst = half_shift(y, S) * S + half_shift(x, S);
+    const float2 ph = tabled ? table[x + y] : shift_phasor(x, y, S, -1.0f);
     const size_t src =
         static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol)
-      sg[pol * npix + dst] =
-          inside ? cmulf(ph, gz[static_cast<size_t>(pol) * G * G + src])
-                 : make_float2(0.0f, 0.0f);
+      store_stream(&sg[pol * npix + dst],
+                   inside ? cmulf(ph, gz[static_cast<size_t>(pol) * G * G + src])
+                          : make_float2(0.0f, 0.0f));
+    x += dx;
+    y += dy;
+    if (x >= S) {
+      x -= S;
+      ++y;
+    }
+  }
+}
+
+// The splitter for S = 32 / 64 (S/2 even): a thread owns PR pixel pairs
+// (x, x + 1) of one row, whose fftshifted destinations are adjacent too
+// (x + S/2 is even, so a pair never straddles the wrap), so each pair is one
+// 16-byte store per correlation; every grid load of the thread is issued
+// before its first store.  The same arithmetic as kernel_splitter.
+template <int S>
+__global__ void __launch_bounds__(256)
+    kernel_splitter_pairs(const idg::Metadata *__restrict__ metadata,
+                          const float2 *__restrict__ grid,
+                          float4 *__restrict__ subgrids, int G,
+                          int nr_w_layers) {
+  static_assert(S % 4 == 0 && (S * S / 2) % 256 == 0, "whole pair rows");
+  constexpr int PR = S * S / 2 / 256;  // pairs per thread
+  constexpr int npix = S * S;
+  __shared__ float2 table[2 * S - 1];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const idg::Metadata m = metadata[s];
+  const bool inside = fits(m, G, S, nr_w_layers);
+  for (int k = tid; k < 2 * S - 1; k += 256)
+    table[k] = unit_phasor(k * (S + 1) - S, 2 * S, -1.0f);
+  __syncthreads();
+  float4 *sg = subgrids + static_cast<size_t>(s) * 4 * npix / 2;
+  if (!inside) {
+#pragma unroll
+    for (int j = 0; j < PR; ++j)
+#pragma unroll
+      for (int pol = 0; pol < 4; ++pol)
+        store_stream(&sg[pol * npix / 2 + tid + 256 * j],
+                     make_float4(0.f, 0.f, 0.f, 0.f));
+    return;
+  }
+  const float2 *gz = grid + static_cast<size_t>(m.coordinate.z) * 4 * G * G;
+  float2 v[PR][4][2];
+#pragma unroll
+  for (int j = 0; j < PR; ++j) {
+    const int p = tid + 256 * j;
+    const int y = p / (S / 2), x = 2 * (p % (S / 2));
+    const size_t src =
+        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+#pragma unroll
+    for (int pol = 0; pol < 4; ++pol) {
+      v[j][pol][0] = gz[static_cast<size_t>(pol) * G * G + src];
+      v[j][pol][1] = gz[static_cast<size_t>(pol) * G * G + src + 1];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PR; ++j) {
+    const int p = tid + 256 * j;
+    const int y = p / (S / 2), x = 2 * (p % (S / 2));
+    const int dst = half_shift(y, S) * S + half_shift(x, S);  // even
+    const float2 p0 = table[x + y], p1 = table[x + 1 + y];
+#pragma unroll
+    for (int pol = 0; pol < 4; ++pol) {
+      const float2 a = cmulf(p0, v[j][pol][0]), b = cmulf(p1, v[j][pol][1]);
+      store_stream(&sg[(pol * npix + dst) / 2],
+                   make_float4(a.x, a.y, b.x, b.y));
+    }
   }
 }
 
@@ -515,8 +622,8 @@ __global__ void __launch_bounds__(128)
     float2 *out = base + static_cast<size_t>(p) * N * N;
 #pragma unroll
     for (int i = 0; i < N; ++i)
-      out[bit_reverse<N>(i) * N + q] =
-          make_float2(x[i].x * scale, x[i].y * scale);
+      store_stream(&out[bit_reverse<N>(i) * N + q],
+                   make_float2(x[i].x * scale, x[i].y * scale));
   }
 }
 
@@ -604,6 +711,15 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
                            const void *d_grid, void *d_subgrids,
                            hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
+  if (subgrid_size == 32 || subgrid_size == 64) {
+    hipLaunchKernelGGL(
+        subgrid_size == 32 ? kernel_splitter_pairs<32> : kernel_splitter_pairs<64>,
+        dim3(nr_subgrids), dim3(256), 0, stream,
+        static_cast<const idg::Metadata *>(d_metadata),
+        static_cast<const float2 *>(d_grid), static_cast<float4 *>(d_subgrids),
+        grid_size, nr_w_layers);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0, stream,
                      static_cast<const idg::Metadata *>(d_metadata),
                      static_cast<const float2 *>(d_grid),
