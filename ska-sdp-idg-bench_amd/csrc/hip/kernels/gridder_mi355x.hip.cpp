@@ -48,6 +48,10 @@
 #ifndef IDG_GRID_WAVES
 #define IDG_GRID_WAVES 4
 #endif
+// general path (w != 0): X + Y in one accumulator tile, 2 PT tiles per wave
+#ifndef IDG_GRID_FUSED_GENERAL
+#define IDG_GRID_FUSED_GENERAL 1
+#endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW
 #define IDG_GRID_NW 8
@@ -221,11 +225,12 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 #endif
 constexpr int kKsBuf = IDG_GRID_KSBUF;  // K-steps (16 items each) of B fragments per fill
 
-// NW waves per workgroup, PT 16-pixel tiles per wave: NW * 16 * PT base
-// pixels per pass, and each B fragment is built once per pass.
-template <int PT, int NW>
+// NW waves per workgroup, AT 16 x 16 accumulator tiles per wave (mirror
+// path: X and Y of PT pixel tiles, AT = 2 PT; general path: one fused X + Y
+// tile per pixel tile, AT = PT).
+template <int AT, int NW>
 struct MfmaLds {
-  static constexpr int kObufFloats = 2 * NW * 16 * PT * 16;  // X and Y tiles
+  static constexpr int kObufFloats = NW * 16 * AT * 16;  // accumulator tiles
   static constexpr int kBbufWords = kKsBuf * 64 * 8;  // uint4 X + uint4 Y
   // uvw of the fill's timesteps (at most 4 * kKsBuf), float4 each
   static constexpr int kUvwOff =
@@ -267,12 +272,18 @@ __device__ __forceinline__ void grid_mfma(
   // MIRROR: base pixels b < npix/2 (mirror npix-1-b shares the phasor);
   // general: every pixel is a base pixel and Y is added, not mirrored.
   const int half = MIRROR ? npix / 2 : npix;
+  // General path: X + Y accumulate into one tile (nothing to mirror), so a
+  // wave holds twice the pixel tiles in the same accumulator registers and
+  // the S = 32 subgrid is one pass (B built once per subgrid, not twice).
+  constexpr bool kFused = !MIRROR && IDG_GRID_FUSED_GENERAL;
+  constexpr int AT = kFused ? PT : 2 * PT;  // accumulator tiles per wave
+  using Lds = MfmaLds<AT, NW>;
   const int nt = g.nr_timesteps;
   const int nchq = (C + 3) / 4;  // channel quads
   const int nquads = (nt + 3) / 4;
   const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
   const int cq_per_fill = nchq <= kKsBuf ? nchq : kKsBuf;
-  unsigned *slots = lds + MfmaLds<PT, NW>::kSlotOff;
+  unsigned *slots = lds + Lds::kSlotOff;
 
   // A power-of-two scale 2^-e keeps the visibilities inside f16 range.  It
   // is set by the maximum over the first fill's timesteps (all channels),
@@ -295,7 +306,7 @@ __device__ __forceinline__ void grid_mfma(
     }
     for (int off = 32; off > 0; off >>= 1)
       vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-    float *red = reinterpret_cast<float *>(lds + MfmaLds<PT, NW>::kRedOff);
+    float *red = reinterpret_cast<float *>(lds + Lds::kRedOff);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();
 #pragma unroll
@@ -311,7 +322,7 @@ __device__ __forceinline__ void grid_mfma(
 
   uint4 *bbuf = reinterpret_cast<uint4 *>(lds);  // [ks][64][X, Y]
   float *obuf = reinterpret_cast<float *>(lds);
-  float4 *tuvw = reinterpret_cast<float4 *>(lds + MfmaLds<PT, NW>::kUvwOff);
+  float4 *tuvw = reinterpret_cast<float4 *>(lds + Lds::kUvwOff);
 
   constexpr int kPass = NW * 16 * PT;  // base pixels per pass
   for (int gbase = 0; gbase < half; gbase += kPass) {
@@ -331,12 +342,12 @@ __device__ __forceinline__ void grid_mfma(
       N2[i / 2][i % 2] = n;
       PG2[i / 2][i % 2] = pg;
     }
-    floatx4 accx[PT], accy[PT];
+    constexpr int PY = kFused ? 1 : PT;  // separate Y tiles (mirror path)
+    floatx4 accx[PT], accy[PY];
 #pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      accx[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-      accy[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
+    for (int i = 0; i < PT; ++i) accx[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < PY; ++i) accy[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 
     for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
       const int nq = min(quads_per_fill, nquads - q0);
@@ -454,10 +465,9 @@ __device__ __forceinline__ void grid_mfma(
         if (have_scale) {
           const float r = ldexpf(1.0f, e - em);
 #pragma unroll
-          for (int i = 0; i < PT; ++i) {
-            accx[i] *= r;
-            accy[i] *= r;
-          }
+          for (int i = 0; i < PT; ++i) accx[i] *= r;
+#pragma unroll
+          for (int i = 0; i < PY; ++i) accy[i] *= r;
         }
         e = em;
         scale = ldexpf(1.0f, -e);
@@ -480,7 +490,7 @@ __device__ __forceinline__ void grid_mfma(
               l2_prefetch_dma(
                   vb + (static_cast<size_t>(4 * q0n + row) * C + 4 * j0n) * 32 +
                       cl * 128,
-                  lds + MfmaLds<PT, NW>::kSinkOff);
+                  lds + Lds::kSinkOff);
             }
           }
         }
@@ -499,6 +509,51 @@ __device__ __forceinline__ void grid_mfma(
             const idg::UVWCoordinate<float> c = {c4.x, c4.y, c4.z};
             const floatx2 cu = {c.u, c.u}, cv = {c.v, c.v};
             const floatx2 ih = {kInv2PiHi, kInv2PiHi};
+            if constexpr (kFused) {
+              // Tile pairs outermost: only one pair's phase terms are live,
+              // and each K-step's B fragments are re-read from LDS per pair.
+#pragma unroll
+              for (int h = 0; h < PH; ++h) {
+                floatx2 pidx = __builtin_elementwise_fma(cu, L2[h], cv * M2[h]);
+                pidx = __builtin_elementwise_fma(floatx2{c.w, c.w}, N2[h], pidx);
+                const floatx2 np = -pidx;
+                const floatx2 a =
+                    __builtin_elementwise_fma(np, floatx2{ka, ka}, PG2[h]);
+                const floatx2 t = a * ih;
+                const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
+#pragma unroll
+                for (int u = 0; u < CB / 4; ++u) {
+                  const int jj = jb + u;
+                  if (jj >= je) break;
+                  const int ks = qq * nj + jj;
+                  const uint4 bx = bbuf[(ks * 64 + lane) * 2];
+                  const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
+                  const half8 bfx = pack4(bx.x, bx.y, bx.z, bx.w);
+                  const half8 bfy = pack4(by.x, by.y, by.z, by.w);
+                  float snx[4], csx[4], sny[4], csy[4];
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) {
+                    const float kj = kb[4 * u + j];
+                    const floatx2 ph =
+                        __builtin_elementwise_fma(np, floatx2{kj, kj}, PG2[h]);
+                    const floatx2 r = __builtin_elementwise_fma(ph, ih, nm);
+                    sincos_rev(r.x, &snx[j], &csx[j]);
+                    sincos_rev(r.y, &sny[j], &csy[j]);
+                  }
+                  half8 ac, as, ac1, as1;
+                  split_oct(csx[0], csx[1], csx[2], csx[3], snx[0], snx[1],
+                            snx[2], snx[3], &ac, &as);
+                  split_oct(csy[0], csy[1], csy[2], csy[3], sny[0], sny[1],
+                            sny[2], sny[3], &ac1, &as1);
+                  accx[2 * h] = mfma16(ac, bfx, accx[2 * h]);
+                  accx[2 * h + 1] = mfma16(ac1, bfx, accx[2 * h + 1]);
+                  accx[2 * h] = mfma16(as, bfy, accx[2 * h]);
+                  accx[2 * h + 1] = mfma16(as1, bfy, accx[2 * h + 1]);
+                  IDG_KSTEP_FENCE();
+                }
+              }
+              continue;
+            }
             floatx2 NP[PH], NM[PH];
 #pragma unroll
             for (int h = 0; h < PH; ++h) {
@@ -574,23 +629,28 @@ __device__ __forceinline__ void grid_mfma(
       for (int r = 0; r < 4; ++r) {
         const int lp = (wave * PT + i) * 16 + grp * 4 + r;
         obuf[lp * 16 + col] = accx[i][r];
-        obuf[(kPass + lp) * 16 + col] = accy[i][r];
+        if constexpr (!kFused) obuf[(kPass + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
     for (int q = tid; q < kPass; q += NW * 64) {
       const int b = gbase + q;
       if (b >= half) continue;
       const float4 *xr = reinterpret_cast<const float4 *>(obuf + q * 16);
-      const float4 *yr =
-          reinterpret_cast<const float4 *>(obuf + (kPass + q) * 16);
       const float4 xh0 = xr[0], xh1 = xr[1], xl0 = xr[2], xl1 = xr[3];
-      const float4 yh0 = yr[0], yh1 = yr[1], yl0 = yr[2], yl1 = yr[3];
       const float x[8] = {xh0.x + xl0.x, xh0.y + xl0.y, xh0.z + xl0.z,
                           xh0.w + xl0.w, xh1.x + xl1.x, xh1.y + xl1.y,
                           xh1.z + xl1.z, xh1.w + xl1.w};
-      const float y[8] = {yh0.x + yl0.x, yh0.y + yl0.y, yh0.z + yl0.z,
-                          yh0.w + yl0.w, yh1.x + yl1.x, yh1.y + yl1.y,
-                          yh1.z + yl1.z, yh1.w + yl1.w};
+      float y[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (!kFused) {  // the Y tiles (fused: already in x)
+        const float4 *yr =
+            reinterpret_cast<const float4 *>(obuf + (kPass + q) * 16);
+        const float4 yh0 = yr[0], yh1 = yr[1], yl0 = yr[2], yl1 = yr[3];
+        const float yv[8] = {yh0.x + yl0.x, yh0.y + yl0.y, yh0.z + yl0.z,
+                             yh0.w + yl0.w, yh1.x + yl1.x, yh1.y + yl1.y,
+                             yh1.z + yl1.z, yh1.w + yl1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = yv[j];
+      }
       // the phase tail of the reduction: base pixel * exp(i poff eps),
       // mirror pixel (phase_offset -poff) * exp(-i poff eps)
       float l, m, n, poff;
@@ -599,7 +659,8 @@ __device__ __forceinline__ void grid_mfma(
       phase_tail(poff, &tc, &ts);
       float ab[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ab[j] = (x[j] + y[j]) * unscale;
+      for (int j = 0; j < 8; ++j)
+        ab[j] = (kFused ? x[j] : x[j] + y[j]) * unscale;
       rotate4(ab, tc, ts);
       store_pixel(ab, b, S, npix, g, nr_stations, spheroidal, aterms, out);
       if constexpr (MIRROR) {
@@ -657,14 +718,16 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 
   if constexpr (MODE == 1) {
     constexpr int NW = IDG_GRID_NW;
-    __shared__ unsigned lds[MfmaLds<PT, NW>::kWords];
+    // both paths hold 2 PT accumulator tiles per wave
+    __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
     if (mirror)
       grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
                                         nr_stations, uvw, wavenumbers,
                                         visibilities, spheroidal, aterms, out,
                                         lds);
     else
-      grid_mfma<S_CT, PT, CB, NW, false>(g, S, npix, image_size, C,
+      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+          g, S, npix, image_size, C,
                                          nr_stations, uvw, wavenumbers,
                                          visibilities, spheroidal, aterms,
                                          out, lds);

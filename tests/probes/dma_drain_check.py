@@ -13,18 +13,29 @@ def check(text):
         if 'global_load_lds' not in f:
             continue
         name = f.split(':')[0]
+        # labels kept (as "LABEL:") so an unconditional s_branch can be
+        # followed: the walk goes in execution order, not listing order
         ins = [l.strip() for l in f.split('\n')
-               if l.strip() and not l.strip().startswith(('.', ';'))]
+               if l.strip() and (not l.strip().startswith(('.', ';'))
+                                 or re.match(r'\.LBB\w+:', l.strip()))]
+        where = {l[:-1]: k for k, l in enumerate(ins) if l.endswith(':')}
         drained = total = 0
         for i, l in enumerate(ins):
             if l.startswith('global_load_lds'):
                 total += 1
-                for j in range(i + 1, len(ins)):
-                    if 'v_mfma' in ins[j]:
+                j, seen = i + 1, set()
+                while j < len(ins) and j not in seen:
+                    seen.add(j)
+                    t = ins[j]
+                    if 'v_mfma' in t:
                         break
-                    if ins[j].startswith('s_waitcnt') and 'vmcnt' in ins[j]:
+                    if t.startswith('s_waitcnt') and 'vmcnt' in t:
                         drained += 1
                         break
+                    if t.startswith('s_branch '):
+                        j = where.get(t.split()[1], len(ins))
+                        continue
+                    j += 1
         scratch = sum(1 for l in ins if l.startswith('scratch_'))
         res.append((name, total, drained, scratch))
     return res
