@@ -2,11 +2,14 @@
 #include "util.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
 #include <memory>
 #include <sstream>
+#include <thread>
+#include <utility>
 
 #include "lib-hip.hpp"
 
@@ -274,6 +277,54 @@ struct DevBuf {
   } while (0)
 }  // namespace
 
+namespace {
+// Visibility row intervals [first, second) of subgrids [s0, s1) in the row
+// space of metadata[0] (the kernels' rebasing, device.hpp:setup_subgrid),
+// merged and sorted.
+std::vector<std::pair<long long, long long>> row_runs(
+    const idg::Metadata *md, int s0, int s1) {
+  std::vector<std::pair<long long, long long>> r;
+  const long long bo0 = md[0].baseline_offset;
+  for (int s = s0; s < s1; ++s) {
+    const long long a = (md[s].baseline_offset - bo0) + md[s].time_offset;
+    if (md[s].nr_timesteps > 0) r.emplace_back(a, a + md[s].nr_timesteps);
+  }
+  std::sort(r.begin(), r.end());
+  std::vector<std::pair<long long, long long>> m;
+  for (const auto &x : r) {
+    if (!m.empty() && x.first <= m.back().second)
+      m.back().second = std::max(m.back().second, x.second);
+    else
+      m.push_back(x);
+  }
+  return m;
+}
+
+struct Stream {
+  hipStream_t s = nullptr;
+  hipError_t create() { return hipStreamCreateWithFlags(&s, hipStreamNonBlocking); }
+  ~Stream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+struct Event {
+  hipEvent_t e = nullptr;
+  hipError_t create() { return hipEventCreateWithFlags(&e, hipEventDisableTiming); }
+  ~Event() {
+    if (e) (void)hipEventDestroy(e);
+  }
+};
+}  // namespace
+
+// The reference's c_run_* contract (app/HIP/util.cpp:255-311: allocate, copy
+// in, launch once, copy out, free) on host buffers.  Large batches are split
+// into chunks of consecutive subgrids whose visibility rows do not overlap:
+// chunk i's input is copied in while chunk i-1 computes, and a second host
+// thread copies chunk i-2's output back meanwhile (pageable copies block the
+// thread that issues them, so each direction gets its own), so the two PCIe
+// directions and the kernel overlap.  The degridder copies back only the
+// rows its subgrids reference, so it need not upload the caller's
+// visibilities to preserve the others.
 hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
                     const void *uvw, const float *wavenumbers,
                     void *visibilities, const float *spheroidal,
@@ -287,15 +338,16 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
   }
   if (p.nr_subgrids == 0) return hipSuccess;
   const size_t S = static_cast<size_t>(p.subgrid_size);
+  const size_t row_b = static_cast<size_t>(p.nr_channels) * 4 * 2 * sizeof(float);
   const size_t b_uvw = e.uvw_rows * 3 * sizeof(float);
   const size_t b_wn = static_cast<size_t>(p.nr_channels) * sizeof(float);
-  const size_t b_vis = e.uvw_rows * p.nr_channels * 4 * 2 * sizeof(float);
+  const size_t b_vis = e.uvw_rows * row_b;
   const size_t b_sph = S * S * sizeof(float);
   const size_t b_at = e.aterm_slots * p.nr_stations * S * S * 4 * 2 *
                       sizeof(float);
   const size_t b_md = static_cast<size_t>(p.nr_subgrids) * sizeof(idg::Metadata);
-  const size_t b_sg = static_cast<size_t>(p.nr_subgrids) * 4 * S * S * 2 *
-                      sizeof(float);
+  const size_t sg_b = 4 * S * S * 2 * sizeof(float);  // one subgrid
+  const size_t b_sg = static_cast<size_t>(p.nr_subgrids) * sg_b;
   DevBuf d_uvw, d_wn, d_vis, d_sph, d_at, d_md, d_sg;
   IDG_TRY(d_uvw.alloc(b_uvw));
   IDG_TRY(d_wn.alloc(b_wn));
@@ -305,25 +357,123 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
   IDG_TRY(d_md.alloc(b_md));
   IDG_TRY(d_sg.alloc(b_sg));
   const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
   IDG_TRY(hipMemcpy(d_uvw.ptr, uvw, b_uvw, h2d));
   IDG_TRY(hipMemcpy(d_wn.ptr, wavenumbers, b_wn, h2d));
   IDG_TRY(hipMemcpy(d_sph.ptr, spheroidal, b_sph, h2d));
   IDG_TRY(hipMemcpy(d_at.ptr, aterms, b_at, h2d));
   IDG_TRY(hipMemcpy(d_md.ptr, metadata, b_md, h2d));
-  // The degridder writes only the rows its subgrids reference; uploading
-  // the caller's buffer first leaves every other row as the caller had it.
-  IDG_TRY(hipMemcpy(d_vis.ptr, visibilities, b_vis, h2d));
-  if (dir == Direction::kDegridder)
-    IDG_TRY(hipMemcpy(d_sg.ptr, subgrids, b_sg, h2d));
-  IDG_TRY(launch(dir, p, d_uvw.ptr, static_cast<const float *>(d_wn.ptr),
-                 d_vis.ptr, static_cast<const float *>(d_sph.ptr), d_at.ptr,
-                 d_md.ptr, d_sg.ptr, nullptr, force));
-  IDG_TRY(hipGetLastError());
-  if (dir == Direction::kGridder)
-    IDG_TRY(hipMemcpy(subgrids, d_sg.ptr, b_sg, hipMemcpyDeviceToHost));
-  else
-    IDG_TRY(hipMemcpy(visibilities, d_vis.ptr, b_vis, hipMemcpyDeviceToHost));
-  return hipDeviceSynchronize();
+
+  // Chunks: ~128 MB of copies each, at most 16, at least 256 subgrids.
+  const bool grid = dir == Direction::kGridder;
+  const size_t moved = b_vis + b_sg;
+  int nchunk = static_cast<int>(std::min<size_t>(16, moved >> 27));
+  nchunk = std::max(1, std::min(nchunk, p.nr_subgrids / 256));
+  std::vector<int> sb(nchunk + 1);
+  std::vector<std::vector<std::pair<long long, long long>>> runs(nchunk);
+  for (int i = 0; i <= nchunk; ++i)
+    sb[i] = static_cast<int>(static_cast<long long>(p.nr_subgrids) * i / nchunk);
+  bool disjoint = true;
+  for (int i = 0; i < nchunk; ++i) {
+    runs[i] = row_runs(metadata, sb[i], sb[i + 1]);
+    if (i > 0 && !runs[i - 1].empty() && !runs[i].empty() &&
+        runs[i].front().first < runs[i - 1].back().second)
+      disjoint = false;
+  }
+  if (!disjoint) {  // one chunk: every row any subgrid reads or writes
+    nchunk = 1;
+    sb = {0, p.nr_subgrids};
+    runs = {row_runs(metadata, 0, p.nr_subgrids)};
+  }
+
+  int dev = 0;
+  IDG_TRY(hipGetDevice(&dev));
+  Stream s_in, s_k, s_out;
+  IDG_TRY(s_in.create());
+  IDG_TRY(s_k.create());
+  IDG_TRY(s_out.create());
+  std::vector<Event> e_in(nchunk), e_k(nchunk);
+  for (int i = 0; i < nchunk; ++i) {
+    IDG_TRY(e_in[i].create());
+    IDG_TRY(e_k[i].create());
+  }
+  char *vis_h = static_cast<char *>(visibilities);
+  char *sg_h = static_cast<char *>(subgrids);
+  char *vis_d = static_cast<char *>(d_vis.ptr);
+  char *sg_d = static_cast<char *>(d_sg.ptr);
+
+  // Output copies on their own thread: chunk i's once its kernel is done.
+  std::atomic<int> launched{0};
+  std::atomic<bool> abort_out{false};
+  hipError_t out_err = hipSuccess;
+  std::thread out([&] {
+    hipError_t err = hipSetDevice(dev);
+    for (int i = 0; i < nchunk && err == hipSuccess; ++i) {
+      while (launched.load(std::memory_order_acquire) <= i) {
+        if (abort_out.load(std::memory_order_acquire)) return;
+        std::this_thread::yield();
+      }
+      err = hipEventSynchronize(e_k[i].e);
+      if (err != hipSuccess) break;
+      if (grid) {
+        const size_t off = static_cast<size_t>(sb[i]) * sg_b;
+        err = hipMemcpyAsync(sg_h + off, sg_d + off,
+                             static_cast<size_t>(sb[i + 1] - sb[i]) * sg_b, d2h,
+                             s_out.s);
+      } else {
+        for (const auto &r : runs[i]) {
+          err = hipMemcpyAsync(vis_h + r.first * row_b, vis_d + r.first * row_b,
+                               static_cast<size_t>(r.second - r.first) * row_b,
+                               d2h, s_out.s);
+          if (err != hipSuccess) break;
+        }
+      }
+      if (err == hipSuccess) err = hipStreamSynchronize(s_out.s);
+    }
+    out_err = err;
+  });
+
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < nchunk && err == hipSuccess; ++i) {
+    // input of chunk i (overlaps chunk i-1's kernel and output copy)
+    if (grid) {
+      for (const auto &r : runs[i]) {
+        err = hipMemcpyAsync(vis_d + r.first * row_b, vis_h + r.first * row_b,
+                             static_cast<size_t>(r.second - r.first) * row_b,
+                             h2d, s_in.s);
+        if (err != hipSuccess) break;
+      }
+    } else {
+      const size_t off = static_cast<size_t>(sb[i]) * sg_b;
+      err = hipMemcpyAsync(sg_d + off, sg_h + off,
+                           static_cast<size_t>(sb[i + 1] - sb[i]) * sg_b, h2d,
+                           s_in.s);
+    }
+    if (err == hipSuccess) err = hipEventRecord(e_in[i].e, s_in.s);
+    if (err == hipSuccess) err = hipStreamWaitEvent(s_k.s, e_in[i].e, 0);
+    if (err == hipSuccess) {
+      // the chunk's metadata starts at sb[i]: the kernels rebase rows on its
+      // first entry, so the row pointers move by that entry's rebase delta
+      Problem pc = p;
+      pc.nr_subgrids = sb[i + 1] - sb[i];
+      const long long delta = static_cast<long long>(metadata[sb[i]].baseline_offset) -
+                              metadata[0].baseline_offset;
+      err = launch(dir, pc,
+                   static_cast<char *>(d_uvw.ptr) + delta * 3 * sizeof(float),
+                   static_cast<const float *>(d_wn.ptr), vis_d + delta * row_b,
+                   static_cast<const float *>(d_sph.ptr), d_at.ptr,
+                   static_cast<const idg::Metadata *>(d_md.ptr) + sb[i],
+                   sg_d + static_cast<size_t>(sb[i]) * sg_b, s_k.s, force);
+    }
+    if (err == hipSuccess) err = hipGetLastError();
+    if (err == hipSuccess) err = hipEventRecord(e_k[i].e, s_k.s);
+    if (err == hipSuccess) launched.store(i + 1, std::memory_order_release);
+  }
+  if (err != hipSuccess) abort_out.store(true, std::memory_order_release);
+  out.join();
+  if (err == hipSuccess) err = out_err;
+  const hipError_t sync = hipDeviceSynchronize();
+  return err != hipSuccess ? err : sync;
 }
 
 double run_performance(Direction dir, const void *func, std::string name,

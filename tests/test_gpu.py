@@ -282,6 +282,52 @@ def test_device_launch_matches_host_entry(idg):
     assert np.array_equal(vis.cpu().numpy(), _degrid(idg, p, a))
 
 
+def test_chunked_host_entry_matches_device_launch(idg):
+    """The host-buffer entries split a batch of >= 256 MB of copies into
+    chunks whose input copy, kernel and output copy overlap (util.cpp
+    run_host).  With ragged and empty subgrids (row gaps) and baseline
+    offsets that move the kernels' row rebasing from chunk to chunk, their
+    outputs equal one device launch over the whole batch bit for bit, and
+    the degridder leaves every row no subgrid references as the caller had
+    it."""
+    import torch
+    st, ts, T, C, G, S = 20, 16, 128, 16, 1024, 32   # 3,040 subgrids, 2 chunks
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    md = a["metadata"].copy()
+    ns = md.size
+    s = np.arange(ns)
+    md["nr_timesteps"] = np.where(s % 7 == 3, 0, np.where(s % 5 == 1, 100, T))
+    md["baseline_offset"] = (s // 97) * 3
+    md["time_offset"] = md["time_offset"] - md["baseline_offset"]
+    p = dict(nr_subgrids=ns, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    dev = _to_device(a)
+    dmd = torch.from_numpy(md.view(np.int32).reshape(-1, 9).copy()).cuda()
+    g_host = np.zeros_like(a["subgrids"])
+    idg.c_run_gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                      a["visibilities"], a["spheroidal"], a["aterms"], md,
+                      g_host)
+    g_dev = torch.zeros_like(dev["subgrids"])
+    idg.gridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                       dev["visibilities"], dev["spheroidal"], dev["aterms"],
+                       dmd, g_dev)
+    torch.cuda.synchronize()
+    assert np.array_equal(g_host, g_dev.cpu().numpy())
+    sentinel = np.float32(7.25)
+    d_host = np.full_like(a["visibilities"], sentinel)
+    idg.c_run_degridder(*_params(p), a["uvw"], a["wavenumbers"], d_host,
+                        a["spheroidal"], a["aterms"], md, a["subgrids"])
+    d_dev = torch.full_like(dev["visibilities"], float(sentinel))
+    idg.degridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], d_dev,
+                         dev["spheroidal"], dev["aterms"], dmd,
+                         dev["subgrids"])
+    torch.cuda.synchronize()
+    d_dev = d_dev.cpu().numpy()
+    assert (d_dev == sentinel).any()  # the gaps exist
+    assert np.array_equal(d_host, d_dev)
+
+
 # --------------------------------------------------------------------------
 # Full BASELINE sizes: size-independent properties + sampled oracle checks
 # --------------------------------------------------------------------------
