@@ -94,6 +94,10 @@ def parse(argv=None):
                     help="must equal the torchrun world size (1 without it)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--min-warmup-s", type=float, default=1.0,
+                    help="continue the untimed warm-up to at least this many "
+                         "seconds of back-to-back steps (clock ramp, "
+                         "DESIGN.md section 6); 0 = exactly --warmup steps")
     ap.add_argument("--workload", default="default", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="sharded",
                     choices=("sharded", "replicated"),
@@ -423,10 +427,13 @@ def upload(part):
     return dev
 
 
-def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None):
-    """warmup untimed steps, then `steps` timed ones bracketed by barrier +
-    synchronize.  Returns (elapsed max over ranks, t_grid, t_degrid (mean
-    per launch, max over ranks), joules, outputs)."""
+def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
+               min_warmup_s=0.0, info=None):
+    """warmup untimed steps (more, up to min_warmup_s of GPU work, see
+    below), then `steps` timed ones bracketed by barrier + synchronize.
+    Returns (elapsed max over ranks, t_grid, t_degrid (mean per launch, max
+    over ranks), joules, outputs); info["warmup_steps_run"] gets the
+    untimed step count."""
     import torch
     import idg_amd
     S, C, G = w["subgrid_size"], w["nr_channels"], w["grid_size"]
@@ -453,11 +460,31 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None):
         if ev:
             ev[2].record(stream)
 
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for _ in range(steps)]
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
-              for _ in range(steps)]
+    # Clock ramp: the device leaves its idle clock state only
+    # after sustained work, and drops back after an idle gap of 20 ms.  A
+    # short shard (3,062 subgrids at N = 8: 2 ms per step) timed after W = 2
+    # warm-up steps ran 10% slower than the same launches after a long
+    # warm-up.  So the untimed warm-up continues for about min_warmup_s of
+    # back-to-back steps (priced by one more step, after the first launches'
+    # one-off costs), the same count on every rank (max over ranks, so that
+    # none idles at the barrier), straight into the timed region.
+    extra = 0
+    if nsub and min_warmup_s > 0:
+        t_w = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        per = max(time.perf_counter() - t_w, 1e-4)
+        extra = 1 + int(min_warmup_s / per)
+    extra = int(dist.max_over_ranks(extra))
+    for _ in range(extra - (1 if nsub and min_warmup_s > 0 else 0)):
+        step()
+    if info is not None:
+        info["warmup_steps_run"] = warmup + extra
     dist.barrier()
     torch.cuda.synchronize()
     if meter:
@@ -592,8 +619,10 @@ def main(argv=None):
 
     from idg_amd.energy import EnergyMeter
     meter = EnergyMeter(local_rank)
+    warm = {}
     elapsed_max, t_grid, t_degrid, joules, elapsed, outs = time_steps(
-        w, dev, nsub, args.steps, args.warmup, stream, dist, meter)
+        w, dev, nsub, args.steps, args.warmup, stream, dist, meter,
+        min_warmup_s=args.min_warmup_s, info=warm)
     sec_per_step = elapsed_max / args.steps
     # visibilities processed per step by all ranks together
     nvis_job = (ns_total * T * C * (world if args.mode == "replicated" else 1))
@@ -674,7 +703,8 @@ def main(argv=None):
         full = upload(shard_batch(a, rank, world, "replicated"))
         wsteps = max(1, min(args.steps, 5))
         w_el, w_tg, w_td, _, _, _ = time_steps(
-            w, full, ns_total, wsteps, 1, stream, dist)
+            w, full, ns_total, wsteps, 1, stream, dist,
+            min_warmup_s=args.min_warmup_s)
         weak = {
             "value": round(world * ns_total * T * C * wsteps / w_el / 1e6, 2),
             "ms_per_step": round(w_el / wsteps * 1e3, 4),
@@ -694,6 +724,7 @@ def main(argv=None):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_steps_run": warm.get("warmup_steps_run", args.warmup),
         "ms_per_step": round(sec_per_step * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak" if args.mode == "replicated" else "strong",
