@@ -14,6 +14,6 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || { echo "pass $i failed"; exit 1; }
+    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || { echo "pass $i failed"; exit 1; }
 done
 echo done

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ktrace" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 10 --warmup 3 --no-cpu-baseline > "$out/bench_ktrace.json"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
-  python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
+  python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --min-warmup-s 0 --no-cpu-baseline > /dev/null
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
-  python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --no-cpu-baseline > /dev/null
+  python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 2 --warmup 1 --min-warmup-s 0 --no-cpu-baseline > /dev/null
 echo done
