@@ -10,7 +10,7 @@ for lib in "$@"; do
   mkdir -p "$root/$n"
   for c in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && export TMPDIR=/tmp && IDG_MI355X_LIB=$GRAFT_REPO_ROOT/$lib timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$root/$n/$c" -o run -- \
-      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-pipeline > /dev/null 2> "$root/$n/$c.err") || { echo "$c failed for $n"; tail -3 "$root/$n/$c.err"; exit 1; }
+      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline --no-pipeline > /dev/null 2> "$root/$n/$c.err") || { echo "$c failed for $n"; tail -3 "$root/$n/$c.err"; exit 1; }
   done
   python3 - "$root/$n" "$n" <<'PY'
 import csv, glob, sys
