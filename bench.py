@@ -427,6 +427,15 @@ def upload(part):
     return dev
 
 
+def extra_warmup_steps(step_s, min_warmup_s):
+    """Untimed steps (the pricing step included) that fill min_warmup_s at
+    step_s seconds per step: at least one, and at most 10,001 (steps priced
+    below 0.1 ms count as 0.1 ms)."""
+    if min_warmup_s <= 0:
+        return 0
+    return 1 + int(min_warmup_s / max(step_s, 1e-4))
+
+
 def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
                min_warmup_s=0.0, info=None):
     """warmup untimed steps (more, up to min_warmup_s of GPU work, see
@@ -478,8 +487,7 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
         t_w = time.perf_counter()
         step()
         torch.cuda.synchronize()
-        per = max(time.perf_counter() - t_w, 1e-4)
-        extra = 1 + int(min_warmup_s / per)
+        extra = extra_warmup_steps(time.perf_counter() - t_w, min_warmup_s)
     extra = int(dist.max_over_ranks(extra))
     for _ in range(extra - (1 if nsub and min_warmup_s > 0 else 0)):
         step()

@@ -232,3 +232,43 @@ def test_bench_shard_batch_uploads_only_its_rows():
         assert np.array_equal(
             p["visibilities"].reshape(n, T, C, 4, 2),
             a["visibilities"][p["s0"]:p["s1"]])
+
+
+# ---------------------------------------------------------------------------
+# bench.py's warm-up: every rank runs the same untimed step count
+# ---------------------------------------------------------------------------
+def _warmup_worker(rank, world, port, out_dir):
+    """Ranks price their step differently (rank r: (2 + r) ms); the count
+    bench.time_steps runs is the max over ranks of extra_warmup_steps."""
+    import sys
+    for p in (PKG, os.path.dirname(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import bench
+    from idg_amd import dist
+    r, _, _ = dist.init(backend="gloo")
+    mine = bench.extra_warmup_steps((2 + r) * 1e-3, 1.0)
+    agreed = int(dist.max_over_ranks(mine))
+    np.save(os.path.join(out_dir, f"r{r}.npy"), np.array([mine, agreed]))
+    dist.finalize()
+
+
+def test_extra_warmup_steps():
+    import bench
+    assert bench.extra_warmup_steps(0.015, 1.0) == 67   # configs[1], N = 1
+    assert bench.extra_warmup_steps(0.002, 1.0) == 501  # N = 8 shard
+    assert bench.extra_warmup_steps(0.0, 1.0) == 10001  # bounded
+    assert bench.extra_warmup_steps(5.0, 1.0) == 1      # the pricing step
+    assert bench.extra_warmup_steps(0.002, 0.0) == 0    # exactly W steps
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_warmup_count_agreed(tmp_path):
+    mp.start_processes(_warmup_worker, args=(2, _free_port(), str(tmp_path)),
+                       nprocs=2, join=True, start_method="spawn")
+    got = [np.load(str(tmp_path / f"r{r}.npy")) for r in range(2)]
+    assert got[0][0] == 501 and got[1][0] == 334
+    assert got[0][1] == got[1][1] == 501
