@@ -501,9 +501,11 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
     for k in range(steps):
         step(events[k])
     torch.cuda.synchronize()
-    joules = meter.stop() if meter else None
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the energy counter is read after the clock stops: an amdsmi call is not
+    # part of the timed steps (its cost would weigh on a 2 ms N = 8 step)
+    joules = meter.stop() if meter else None
     elapsed_max = dist.max_over_ranks(elapsed)
     if nsub:
         t_grid = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3

@@ -56,14 +56,16 @@ def main():
                             -1, C, 4, 2)[r0:r1].copy(),
                         subgrids=a["subgrids"][:n].copy())
             dev = bench.upload(part)
-            _, tg, td, _, _, _ = bench.time_steps(
+            el, tg, td, _, _, _ = bench.time_steps(
                 w, dev, n, args.steps, args.warmup, stream, dist,
                 min_warmup_s=args.min_warmup_s)
             del dev
             torch.cuda.empty_cache()
             print(json.dumps({"nr_subgrids": n,
                               "gridder_ms": round(tg * 1e3, 4),
-                              "degridder_ms": round(td * 1e3, 4)}),
+                              "degridder_ms": round(td * 1e3, 4),
+                              "wall_ms_per_step": round(
+                                  el / args.steps * 1e3, 4)}),
                   flush=True)
         return
     rows, base = [], None
@@ -74,7 +76,7 @@ def main():
             part = bench.shard_batch(a, rank, world)
             nsub = part["s1"] - part["s0"]
             dev = bench.upload(part)
-            _, tg, td, _, _, _ = bench.time_steps(
+            el, tg, td, _, _, _ = bench.time_steps(
                 w, dev, nsub, args.steps, args.warmup, stream, dist,
                 min_warmup_s=args.min_warmup_s)
             del dev
@@ -84,7 +86,9 @@ def main():
             rows.append({"world": world, "rank": rank, "nr_subgrids": nsub,
                          "gridder_ms": round(tg * 1e3, 4),
                          "degridder_ms": round(td * 1e3, 4),
-                         "step_ms": round(step * 1e3, 4)})
+                         "step_ms": round(step * 1e3, 4),
+                         "wall_ms_per_step": round(
+                             el / args.steps * 1e3, 4)})
             print(json.dumps(rows[-1]), flush=True)
         if base is None:
             base = worst
