@@ -244,6 +244,10 @@ double idg_p_run_degridder(void) {
   idg_mi355x::Problem p;
   p.subgrid_size = static_cast<int>(get_env_var("SUBGRID_SIZE", 32));
   p.nr_channels = static_cast<int>(get_env_var("NR_CHANNELS", 16));
+  // the batch run_performance builds (the kernel choice depends on its size)
+  const int nr_stations = static_cast<int>(get_env_var("NR_STATIONS", 50));
+  p.nr_subgrids = nr_stations * (nr_stations - 1) / 2 *
+                  static_cast<int>(get_env_var("NR_TIMESLOTS", 20));
   const auto k = idg_mi355x::select_degridder(p);
   return 1e3 * idg_mi355x::run_performance(idg_mi355x::Direction::kDegridder,
                                            k.func, "degridder_mi355x",
