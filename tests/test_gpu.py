@@ -613,6 +613,33 @@ def test_full_size_deterministic_and_shard_invariant(idg, full):
     assert torch.equal(torch.cat(parts), g)
 
 
+def test_full_size_degridder_shard_invariant_across_workgroup_shapes(idg,
+                                                                     full):
+    """The full batch (24,500 subgrids: 4-wave degridder workgroups) and its
+    8 shards of 3,062-3,063 subgrids (below 4,096: 8-wave workgroups,
+    select_degridder) degrid to bitwise identical visibilities."""
+    import torch
+    from idg_amd import shard
+    p, a, dev = full
+    v = _ddegrid(idg, p, dev, dev["subgrids"])
+    C = p["nr_channels"]
+    parts = []
+    for s0, s1 in shard.plan_shards(a["metadata"], 8):
+        assert s1 - s0 < 4096
+        md, r0, r1 = shard.shard(a["metadata"], s0, s1)
+        q = dict(p, nr_subgrids=s1 - s0)
+        sub = {"uvw": dev["uvw"].reshape(-1, 3)[r0:r1].contiguous(),
+               "wavenumbers": dev["wavenumbers"],
+               "spheroidal": dev["spheroidal"], "aterms": dev["aterms"],
+               "metadata": torch.from_numpy(
+                   md.view(np.int32).reshape(-1, 9).copy()).cuda(),
+               "visibilities": dev["visibilities"].reshape(
+                   -1, C, 4, 2)[r0:r1].contiguous()}
+        parts.append(_ddegrid(idg, q, sub, dev["subgrids"][s0:s1].contiguous())
+                     .reshape(-1, C, 4, 2))
+    assert torch.equal(torch.cat(parts), v.reshape(-1, C, 4, 2))
+
+
 # --------------------------------------------------------------------------
 # The reference-style harness executables (hip-<kernel> -c)
 # --------------------------------------------------------------------------
