@@ -129,6 +129,17 @@ int idg_validate_metadata(int nr_subgrids, int subgrid_size, int nr_channels,
                           int nr_stations, size_t uvw_rows, size_t aterm_slots,
                           const idg_metadata_t *metadata);
 
+/* The chunk plan the host-buffer entries use for a batch whose copies move
+ * bytes_moved bytes (visibilities + subgrids): consecutive subgrid ranges
+ * [bounds[i], bounds[i+1]) whose visibility rows are disjoint and ascending,
+ * so chunk i's copies overlap chunk i-1's kernel; one chunk when the rows are
+ * not.  Writes at most max_bounds entries of bounds (nchunk + 1 in all) and
+ * returns nchunk (< 0 on bad arguments).  No reference counterpart: the
+ * reference's c_run_* copies everything, launches once, copies back
+ * (app/HIP/util.cpp:255-311). */
+int idg_host_chunk_plan(int nr_subgrids, const idg_metadata_t *metadata,
+                        size_t bytes_moved, int *bounds, int max_bounds);
+
 /* Name of the kernel the launch entries select for this geometry
  * (direction 0 = gridder, 1 = degridder); for profiles and reports. */
 const char *idg_kernel_name(int direction, int subgrid_size, int nr_channels);

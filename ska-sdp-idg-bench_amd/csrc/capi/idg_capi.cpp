@@ -223,6 +223,20 @@ int idg_validate_metadata(int nr_subgrids, int subgrid_size, int nr_channels,
   return IDG_OK;
 }
 
+int idg_host_chunk_plan(int nr_subgrids, const idg_metadata_t *metadata,
+                        size_t bytes_moved, int *bounds, int max_bounds) {
+  if (nr_subgrids <= 0 || metadata == nullptr)
+    return fail(IDG_E_INVALID_ARGUMENT, "nr_subgrids <= 0 or null metadata");
+  std::vector<int> sb;
+  const int n = idg_mi355x::plan_host_chunks(
+      reinterpret_cast<const idg::Metadata *>(metadata), nr_subgrids,
+      bytes_moved, &sb, nullptr);
+  if (bounds)
+    for (int i = 0; i < static_cast<int>(sb.size()) && i < max_bounds; ++i)
+      bounds[i] = sb[i];
+  return n;
+}
+
 const char *idg_kernel_name(int direction, int subgrid_size, int nr_channels) {
   idg_mi355x::Problem p;
   p.subgrid_size = subgrid_size;

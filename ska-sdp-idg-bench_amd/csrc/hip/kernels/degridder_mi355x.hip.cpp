@@ -3,7 +3,8 @@
 // Replaces the reference's app/HIP/kernels/degridder_*.hip.cpp behind the same
 // kernel-TU contract (hip::p_run_degridder, hip::c_run_degridder; harness
 // declarations tests/degridder_common.cpp:13-31) and 13-argument kernel ABI
-// (grid = nr_subgrids, block = 256 = 4 wave64).  It computes
+// (grid = nr_subgrids; block = 256 = 4 wave64, or 512 = 8 wave64 for
+// launches below kDegridSmallLaunch subgrids, select_degridder).  It computes
 // cpu::kernel_degridder_reference
 // (app/CPU/kernels/degridder_reference.cpp:6-129):
 //
@@ -179,7 +180,7 @@ __device__ __forceinline__ void degrid_mfma(
     const float2 *__restrict__ sg, unsigned *lds) {
   static_assert(CT % CB == 0 && CB % 2 == 0,
                 "channel tiles hold whole, even anchor blocks");
-  static_assert(KP % 32 == 0, "chunks hold whole K-steps for 4 waves");
+  static_assert(KP % 32 == 0, "chunks hold whole 8-pair K-steps, 4 per pass");
   using L = DegridMfmaLds<KP>;
   constexpr int kThreads = 64 * NW;
   const int tid = threadIdx.x;

@@ -245,16 +245,24 @@ struct MfmaLds {
 // lds_dst + 4 * lane (lds_dst wave-uniform), as inline asm: the gridder uses
 // it only to pull the next fill's rows into L2 (the LDS words are a sink
 // nobody reads), and hipcc, which cannot see the asm, inserts no wait for
-// it; every __syncthreads() drains it (s_waitcnt vmcnt(0)).
+// it; every __syncthreads() drains it (s_waitcnt vmcnt(0)).  M0 is a
+// reserved register the compiler manages itself (a clobber of it is
+// ignored), so the asm saves and restores it around its own use; and the
+// SALU write of M0 is followed by one wait state before the LDS-DMA reads
+// it (the gfx9 "M0 write -> LDS DMA" hazard, which the compiler cannot pad
+// inside an asm string; tests/probes/dma_drain_check.py checks the listing).
 __device__ __forceinline__ void l2_prefetch_dma(const void *src,
                                                 const void *lds_dst) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(
       reinterpret_cast<size_t>((const __attribute__((address_space(3))) void *)
                                    lds_dst)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off"
-               :
-               : "v"(src), "s"(m0)
-               : "memory");
+  unsigned saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(src), "s"(m0)
+      : "memory");
 }
 
 template <int S_CT, int PT, int CB, int NW, bool MIRROR>

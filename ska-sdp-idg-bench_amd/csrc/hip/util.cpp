@@ -316,6 +316,40 @@ struct Event {
 };
 }  // namespace
 
+int plan_host_chunks(const idg::Metadata *metadata, int nr_subgrids,
+                     size_t moved, std::vector<int> *bounds,
+                     std::vector<std::vector<std::pair<long long, long long>>>
+                         *row_runs_out) {
+  std::vector<int> sb;
+  std::vector<std::vector<std::pair<long long, long long>>> runs;
+  int nchunk = static_cast<int>(std::min<size_t>(16, moved >> 27));
+  nchunk = std::max(1, std::min(nchunk, nr_subgrids / 256));
+  sb.resize(nchunk + 1);
+  runs.resize(nchunk);
+  for (int i = 0; i <= nchunk; ++i)
+    sb[i] = static_cast<int>(static_cast<long long>(nr_subgrids) * i / nchunk);
+  // Chunks must be disjoint AND ascending in rows: each chunk's first row
+  // is compared with the largest row end of EVERY earlier chunk (a chunk
+  // with no rows, e.g. only zero-timestep subgrids, must not hide an
+  // overlap between its neighbours).
+  bool disjoint = true;
+  long long row_end = -1;  // max row end over the chunks so far
+  for (int i = 0; i < nchunk; ++i) {
+    runs[i] = row_runs(metadata, sb[i], sb[i + 1]);
+    if (runs[i].empty()) continue;
+    if (runs[i].front().first < row_end) disjoint = false;
+    row_end = std::max(row_end, runs[i].back().second);
+  }
+  if (!disjoint) {  // one chunk: every row any subgrid reads or writes
+    nchunk = 1;
+    sb = {0, nr_subgrids};
+    runs = {row_runs(metadata, 0, nr_subgrids)};
+  }
+  if (bounds) *bounds = std::move(sb);
+  if (row_runs_out) *row_runs_out = std::move(runs);
+  return nchunk;
+}
+
 // The reference's c_run_* contract (app/HIP/util.cpp:255-311: allocate, copy
 // in, launch once, copy out, free) on host buffers.  Large batches are split
 // into chunks of consecutive subgrids whose visibility rows do not overlap:
@@ -366,25 +400,10 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
 
   // Chunks: ~128 MB of copies each, at most 16, at least 256 subgrids.
   const bool grid = dir == Direction::kGridder;
-  const size_t moved = b_vis + b_sg;
-  int nchunk = static_cast<int>(std::min<size_t>(16, moved >> 27));
-  nchunk = std::max(1, std::min(nchunk, p.nr_subgrids / 256));
-  std::vector<int> sb(nchunk + 1);
-  std::vector<std::vector<std::pair<long long, long long>>> runs(nchunk);
-  for (int i = 0; i <= nchunk; ++i)
-    sb[i] = static_cast<int>(static_cast<long long>(p.nr_subgrids) * i / nchunk);
-  bool disjoint = true;
-  for (int i = 0; i < nchunk; ++i) {
-    runs[i] = row_runs(metadata, sb[i], sb[i + 1]);
-    if (i > 0 && !runs[i - 1].empty() && !runs[i].empty() &&
-        runs[i].front().first < runs[i - 1].back().second)
-      disjoint = false;
-  }
-  if (!disjoint) {  // one chunk: every row any subgrid reads or writes
-    nchunk = 1;
-    sb = {0, p.nr_subgrids};
-    runs = {row_runs(metadata, 0, p.nr_subgrids)};
-  }
+  std::vector<int> sb;
+  std::vector<std::vector<std::pair<long long, long long>>> runs;
+  const int nchunk =
+      plan_host_chunks(metadata, p.nr_subgrids, b_vis + b_sg, &sb, &runs);
 
   int dev = 0;
   IDG_TRY(hipGetDevice(&dev));

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "lib-common.hpp"
@@ -138,6 +139,15 @@ hipError_t run_host(Direction dir, const Problem &p, const Extents &e,
                     const void *aterms, const idg::Metadata *metadata,
                     void *subgrids, std::string *msg,
                     const KernelChoice *force = nullptr);
+
+// Chunk plan of run_host: subgrid bounds (nchunk + 1 entries) of
+// consecutive chunks whose visibility rows are disjoint and ascending, and
+// each chunk's merged row runs; one chunk when they are not.  `moved` =
+// bytes of visibilities + subgrids.  Returns the chunk count.
+int plan_host_chunks(const idg::Metadata *metadata, int nr_subgrids,
+                     size_t moved, std::vector<int> *bounds,
+                     std::vector<std::vector<std::pair<long long, long long>>>
+                         *row_runs);
 
 // Pipeline steps (kernels/pipeline_mi355x.hip.cpp; include/idg_mi355x.h).
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,

@@ -34,6 +34,7 @@ SIGNATURES = {
     "idg_degridder_launch": (_I, [_I, _I, _I, _F, _F, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _P, _P]),
     "idg_validate_metadata": (_I, [_I, _I, _I, _I, _Z, _Z, _P]),
+    "idg_host_chunk_plan": (_I, [_I, _P, _Z, _P, _I]),
     "idg_kernel_name": (_S, [_I, _I, _I]),
     "idg_p_run_gridder": (_D, []),
     "idg_p_run_degridder": (_D, []),

@@ -175,6 +175,22 @@ def validate_metadata(nr_subgrids, subgrid_size, nr_channels, nr_stations,
         "validate_metadata")
 
 
+def host_chunk_plan(metadata, bytes_moved):
+    """Subgrid bounds of the chunks the host-buffer entries split a batch
+    into (idg_host_chunk_plan; util.cpp plan_host_chunks): a list of
+    nchunk + 1 subgrid indices."""
+    import numpy as np
+    md = as_metadata(metadata)
+    bounds = np.zeros(18, np.int32)
+    n = lib.idg_host_chunk_plan(md.size, _np_ptr(md, METADATA_DTYPE,
+                                                  "metadata"),
+                                int(bytes_moved), bounds.ctypes.data_as(
+                                    ctypes.c_void_p), bounds.size)
+    if n < 0:
+        _check(n, "host_chunk_plan")
+    return [int(b) for b in bounds[:n + 1]]
+
+
 # ---------------------------------------------------------------------------
 # Device-buffer entries (torch CUDA tensors, asynchronous on a stream)
 # ---------------------------------------------------------------------------

@@ -14,7 +14,7 @@ for lib in "$@"; do
              "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     (cd /tmp && export TMPDIR=/tmp && IDG_MI355X_LIB=$GRAFT_REPO_ROOT/$lib timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$root/$n/p$i" -o run -- \
-      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-pipeline > /dev/null 2> "$root/$n/p$i.err") || { echo "pass $i failed for $n"; tail -3 "$root/$n/p$i.err"; exit 1; }
+      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline --no-pipeline > /dev/null 2> "$root/$n/p$i.err") || { echo "pass $i failed for $n"; tail -3 "$root/$n/p$i.err"; exit 1; }
   done
   python3 - "$root/$n" <<'PY'
 import csv, glob, sys

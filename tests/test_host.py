@@ -190,3 +190,35 @@ def test_shard_handles_baseline_offsets():
     sub, row0, row1 = shard.shard(md, 2, 4)
     assert (row0, row1) == (10, 20)
     assert list(sub["time_offset"]) == [0, 5]
+
+
+def _chunk_md(ns, T=128):
+    md = np.zeros(ns, dtype=idg_amd.METADATA_DTYPE)
+    md["time_offset"] = np.arange(ns) * T
+    md["nr_timesteps"] = T
+    return md
+
+
+def test_host_chunk_plan_splits_disjoint_rows():
+    # 6,080 subgrids, ~600 MB of copies -> 4 chunks of 1,520
+    md = _chunk_md(6080)
+    assert idg_amd.host_chunk_plan(md, 600 << 20) == [0, 1520, 3040, 4560,
+                                                       6080]
+    # small batches stay one chunk
+    assert idg_amd.host_chunk_plan(md, 100 << 20) == [0, 6080]
+
+
+def test_host_chunk_plan_empty_middle_chunk_does_not_hide_an_overlap():
+    # chunk 1 has only zero-timestep subgrids; chunk 2 reads the
+    # rows of chunk 0.  Comparing only neighbours missed that overlap (the
+    # degridder's chunk-0 copy-back would race chunk 2's kernel); the plan
+    # must fall back to one chunk.
+    md = _chunk_md(6080)
+    md["nr_timesteps"][1520:3040] = 0
+    md["time_offset"][3040:4560] = md["time_offset"][0:1520]
+    assert idg_amd.host_chunk_plan(md, 600 << 20) == [0, 6080]
+    # an empty middle chunk with ascending rows either side still splits
+    md = _chunk_md(6080)
+    md["nr_timesteps"][1520:3040] = 0
+    assert idg_amd.host_chunk_plan(md, 600 << 20) == [0, 1520, 3040, 4560,
+                                                       6080]

@@ -116,3 +116,26 @@ def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
     assert mfma_kernels, "no gridder kernel with an LDS-DMA prefetch"
     for name, total, drained, _ in mfma_kernels:
         assert total > 0 and drained == 0, (name[:60], total, drained)
+
+
+def test_lds_dma_m0_wait_state_checker():
+    import dma_drain_check as ddc
+    src = """
+_Zk:
+\ts_mov_b32 m0, s5
+{pad}\tglobal_load_lds_dword v[2:3], off
+\ts_endpgm
+"""
+    bad = ddc.check(src.format(pad=""), with_m0=True)
+    ok = ddc.check(src.format(pad="\ts_nop 0\n"), with_m0=True)
+    assert bad[0][4] == 1 and ok[0][4] == 0
+
+
+def test_shipped_lds_dma_has_m0_wait_state(listings):
+    # ADVICE r02: the asm's SALU write of M0 needs one wait state before the
+    # LDS-DMA that reads it; the compiler cannot pad inside the asm string.
+    import dma_drain_check as ddc
+    res = ddc.check(open(listings["gridder"]).read(), with_m0=True)
+    assert res, "no kernel with an LDS-DMA"
+    for name, total, _, _, m0 in res:
+        assert total > 0 and m0 == 0, (name[:60], total, m0)
