@@ -21,16 +21,26 @@ over ranks of the timed region (strong scaling).  The per-rank full-batch
 
 `value` counts a visibility once per step (it is gridded AND degridded);
 per-kernel Mvis/s are reported alongside.  `roofline` is for the dominant
-(slower) kernel -- see roofline_for() and DESIGN.md §4.3: the kernels are
-bound by vector-issue cycles (exact phase, v_sin/v_cos, f16 operand split,
-MFMA issue), so `frac` is the measured time's share of that issue ceiling,
-and the f16-MFMA and FP32-equivalent views are reported beside it.
+(slower) kernel -- see roofline_for() and DESIGN.md §4.3: the hardware floor
+is the transcendental unit (v_sin + v_cos of the reference's exact f32 phase
+for every phasor), so `frac` is that floor's time over the measured time;
+the kernel's issue efficiency (its own instruction stream at the measured
+issue costs), the f16-MFMA and the FP32-equivalent views sit beside it.
 cpu_baseline times the reference's own CPU path (oracle/_ref) on a bounded
 sample of the same batch, on the host cores this process may use and on one
 thread as the reference builds it.
 
     python bench.py [--gpus N --steps K --warmup W] [--workload default]
                     [--mode sharded|replicated] [--dump DIR]
+
+`--gpus N` with N > 1 works both under torchrun (one rank per GPU, RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* from the environment) and as a plain
+command: without WORLD_SIZE the process touches no device, starts
+`torch.distributed.run --nproc-per-node N` on itself as a child (rendezvous
+on 127.0.0.1), and exits with its exit code (non-zero if any rank failed);
+rank 0's JSON line is the output.  `--plan-only` stops each rank after the
+rendezvous and the shard plan (no device needed: the launcher and sharding
+rehearsed on CPU with IDG_DIST_BACKEND=gloo, tests/test_distributed.py).
 """
 import argparse
 import json
@@ -119,7 +129,31 @@ def parse(argv=None):
                          "(.npy; tests/test_gpu_dist.py)")
     ap.add_argument("--traffic-file", default=os.path.join(
         REPO, "profiles", "traffic.json"))
+    ap.add_argument("--plan-only", action="store_true",
+                    help="rendezvous, shard the batch and print the plan "
+                         "line (value null); no device is touched")
     return ap.parse_args(argv)
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) run as a plain command: start one rank per GPU
+    with torch.distributed.run as a CHILD process (never exec: the parent
+    has not touched the GPU, and on this pool a process that has must not
+    be replaced) and return its exit code, which is non-zero when any rank
+    failed.  The ranks inherit stdout, so rank 0's JSON line is this
+    command's output."""
+    import socket
+    import subprocess
+    argv = list(sys.argv[1:] if argv is None else argv)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
 
 
 # ---------------------------------------------------------------------------
@@ -340,67 +374,90 @@ def profile_entry(path, workload_name, kernel):
         return None
 
 
-def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled):
+def transcendental_floor(w, nsub):
+    """(wave-instructions, seconds) of the v_sin/v_cos a launch over nsub
+    subgrids cannot avoid: one exact f32 phase per (pixel, timestep,
+    channel) and its sin and cos (the reference's own arithmetic, §3), one
+    pair per mirror pair of pixels where the pairing applies (even S, w = 0:
+    every workload but 'wterm'), at the measured 8.35 cycles per wave64
+    transcendental on each of the 1,024 SIMDs (profiles/r02/rates/)."""
+    S, T, C = w["subgrid_size"], w["nr_timesteps"], w["nr_channels"]
+    mirror = S % 2 == 0 and not w.get("w_range")
+    pixels = S * S // 2 if mirror else S * S
+    insts = 2.0 * nsub * pixels * T * C / 64
+    return insts, insts * ISSUE_CYC["trans"] / NR_SIMDS / CLOCK_HZ
+
+
+def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled,
+                 w=None):
     """Roofline of the dominant kernel.
 
-    The kernels are bound by vector issue: per phasor, the exact fp32 phase,
-    v_sin + v_cos, the two-term f16 split of the MFMA operand and half an
-    f16 MFMA, all issued by the same SIMD.  The ceiling is the time the
-    kernel's own instruction stream needs at full issue rate:
-        t_issue = (trans x 8.35 + mfma_f16 x 4.7 + other VALU x 4.46) cycles
-                  / 1024 SIMDs / 2.4 GHz
-    from the per-launch wave-instruction counts of the committed SQ profile
-    (profiles/traffic.json -> issue_bound; scaled by subgrids when this
-    launch grids a shard) and the measured issue costs
-    (tests/probes/instr_rates_probe.hip).  achieved = the reference work model's
-    FLOPs (app/common/common.cpp:100-129) / measured time; peak = the same
-    FLOPs / t_issue; frac = t_issue / t <= 1.  Beside it: executed f16 MFMA
-    FLOP/s against the dense f16 peak (mfma), and the work model against the
-    FP32 peak the reference prices it on (fp32_equivalent; > 1 because the
-    complex MAC runs on the f16 matrix core)."""
+    The binding hardware resource is the transcendental unit: every
+    phasor needs v_sin + v_cos of the reference's exact f32 phase (quarter
+    rate, 8.35 cycles per wave64 instruction), and nothing else the path
+    must do is as scarce.  So
+        t_floor = 2 x phasors / 64 x 8.35 cycles / 1024 SIMDs / 2.4 GHz
+    (transcendental_floor), achieved = the reference work model's FLOPs
+    (app/common/common.cpp:100-129) / measured time, peak = the same FLOPs
+    / t_floor, frac = t_floor / t.  Beside it:
+      mfma             the work model against the dense f16 MFMA peak, and
+                       the MFMA FLOPs actually executed (two-term split);
+      issue_efficiency the kernel's own instruction stream at the measured
+                       issue costs over its time (how well it issues what it
+                       has; from the committed SQ profile,
+                       profiles/traffic.json -> issue_bound);
+      fp32_equivalent  the work model against the FP32 peak the reference
+                       prices it on (> 1: the MAC runs on the matrix core)."""
     achieved = flops / t / 1e12
     out = {"bound": "mfma", "achieved": round(achieved, 3),
-           "unit": "TFLOP/s", "kernel": kernel,
-           "traffic": None}
-    ib = (entry or {}).get("issue_bound")
+           "unit": "TFLOP/s", "kernel": kernel, "traffic": None}
     scale = nsub_launch / nsub_profiled if nsub_profiled else 1.0
     if entry and entry.get("hbm_bytes_per_launch"):
         out["traffic"] = int(entry["hbm_bytes_per_launch"] * scale)
+    if w is not None:
+        trans, t_floor = transcendental_floor(w, nsub_launch)
+        out.update({
+            "resource": "transcendental issue (v_sin + v_cos of the "
+                        "reference's exact f32 phase, one pair per phasor)",
+            "peak": round(flops / t_floor / 1e12, 3),
+            "frac": round(t_floor / t, 4),
+            "floor": {"t_floor_ms": round(t_floor * 1e3, 4),
+                      "trans_wave_insts": trans,
+                      "cycles_per_trans": ISSUE_CYC["trans"],
+                      "simds": NR_SIMDS, "clock_ghz": CLOCK_HZ / 1e9},
+        })
+    out["mfma"] = {
+        "work_model_frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
+        "peak": F16_MFMA_PEAK_TFLOPS,
+        "note": "the reference work model's FLOPs over the measured time "
+                "against the dense f16 MFMA peak"}
+    ib = (entry or {}).get("issue_bound")
     if ib and ib.get("insts_valu"):
-        trans = ib["insts_trans"] * scale
+        trans_i = ib["insts_trans"] * scale
         mfma = ib["insts_mfma_f16"] * scale
-        other = ib["insts_valu"] * scale - trans - mfma
-        cyc = (trans * ISSUE_CYC["trans"] + mfma * ISSUE_CYC["mfma_f16"] +
+        other = ib["insts_valu"] * scale - trans_i - mfma
+        cyc = (trans_i * ISSUE_CYC["trans"] + mfma * ISSUE_CYC["mfma_f16"] +
                other * ISSUE_CYC["other"]) / NR_SIMDS
         t_issue = cyc / CLOCK_HZ
-        peak = flops / t_issue / 1e12
-        out.update({
-            "resource": "vector issue per SIMD (v_sin/v_cos + VALU + f16 "
-                        "MFMA issue cycles of the kernel's own instruction "
-                        "stream)",
-            "peak": round(peak, 3),
+        out["issue_efficiency"] = {
             "frac": round(t_issue / t, 4),
-            "issue_model": {
-                "t_issue_ms": round(t_issue * 1e3, 4),
-                "insts_per_launch": {"trans": trans, "mfma_f16": mfma,
-                                     "other_valu": other},
-                "cycles": ISSUE_CYC, "clock_ghz": CLOCK_HZ / 1e9,
-                "source": ib.get("source"),
-            },
-        })
+            "t_issue_ms": round(t_issue * 1e3, 4),
+            "insts_per_launch": {"trans": trans_i, "mfma_f16": mfma,
+                                 "other_valu": other},
+            "cycles": ISSUE_CYC, "clock_ghz": CLOCK_HZ / 1e9,
+            "source": ib.get("source"),
+            "note": "the kernel's own instruction stream (SQ counters) at "
+                    "the measured issue costs, over the measured time"}
         mfma_tf = mfma * MFMA_F16_FLOP / t / 1e12
-        out["mfma"] = {"achieved": round(mfma_tf, 3),
-                       "peak": F16_MFMA_PEAK_TFLOPS,
-                       "frac": round(mfma_tf / F16_MFMA_PEAK_TFLOPS, 4),
-                       "note": "executed v_mfma_f32_16x16x32_f16 FLOPs "
-                               "(two-term split: 4 f16 products per f32 "
-                               "MAC) / measured time"}
-    else:
-        # no committed counters for this workload: the dense f16 MFMA peak
+        out["mfma"].update({
+            "executed_tflops": round(mfma_tf, 3),
+            "executed_frac": round(mfma_tf / F16_MFMA_PEAK_TFLOPS, 4),
+            "executed_note": "v_mfma_f32_16x16x32_f16 FLOPs executed (two-"
+                             "term split: 4 f16 products per f32 MAC)"})
+    if "frac" not in out:
         out.update({"peak": F16_MFMA_PEAK_TFLOPS,
                     "frac": round(achieved / F16_MFMA_PEAK_TFLOPS, 4),
-                    "resource": "f16 MFMA dense peak (no SQ profile of this "
-                                "workload committed)"})
+                    "resource": "f16 MFMA dense peak"})
     out["fp32_equivalent"] = {
         "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
         "ratio": round(achieved / FP32_PEAK_TFLOPS, 4),
@@ -408,8 +465,9 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled):
                 "because its complex MAC runs on the f16 matrix core"}
     out["note"] = (f"achieved = reference work model {flops / nvis:.0f} "
                    f"FLOP/vis x {nvis} vis per launch / mean kernel duration "
-                   "(HIP events on the launch stream); frac = issue-model "
-                   "time / measured time (DESIGN.md §4.3)")
+                   "(HIP events on the launch stream); peak = the same FLOPs "
+                   "at the transcendental floor; frac = t_floor / t "
+                   "(DESIGN.md §4.3)")
     return out
 
 
@@ -595,18 +653,55 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
     return out, gridt
 
 
+def plan_line(args, w, a, world, dist):
+    """The --plan-only line: the rendezvous and shard plan of a run, no
+    device work (value null)."""
+    counts = shard_counts(a, world, args.mode)
+    T, C = w["nr_timesteps"], w["nr_channels"]
+    ranks = dist.sum_over_ranks(1.0)  # a collective over every rank
+    return {
+        "metric": METRIC, "value": None, "unit": "Mvis/s", "n_gpus": world,
+        "plan_only": True, "ranks_in_collective": int(ranks),
+        "scaling": "weak" if args.mode == "replicated" else "strong",
+        "config": {"workload": args.workload,
+                   "nr_subgrids": int(a["metadata"].size),
+                   "nr_subgrids_per_gpu": counts,
+                   "visibilities_per_step": int(
+                       a["metadata"].size * T * C *
+                       (world if args.mode == "replicated" else 1)),
+                   "backend": dist.backend_name()},
+    }
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a plain `python bench.py --gpus N`: become the launcher
+        raise SystemExit(launch_ranks(args, argv))
     import numpy as np
     import torch
     import idg_amd
     from idg_amd import dist
 
+    if args.plan_only:
+        rank, _, world = dist.init(
+            backend=os.environ.get("IDG_DIST_BACKEND", "gloo"))
+        w = workload(args.workload, args.timeslots)
+        a = make_batch(w, nthreads=max(1, min(8, (os.cpu_count() or 8)
+                                              // max(1, world))))
+        line = plan_line(args, w, a, world, dist)
+        if args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the world "
+                             f"size is {world}")
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        dist.finalize()
+        return line
+
     rank, local_rank, world = dist.init()
     if args.gpus != world:
         raise SystemExit(
-            f"bench.py: --gpus {args.gpus} but the world size is {world}; "
-            "launch N>1 under torchrun (--nproc-per-node N)")
+            f"bench.py: --gpus {args.gpus} but the world size is {world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     torch.cuda.set_device(local_rank)
@@ -657,7 +752,7 @@ def main(argv=None):
     entry = profile_entry(args.traffic_file, args.workload,
                           kernels[dom]["kernel"])
     roofline = roofline_for(entry, kernels[dom]["kernel"], flops, nvis_max,
-                            t_dom, nsub_max, ns_total if entry else 0)
+                            t_dom, nsub_max, ns_total if entry else 0, w)
     if entry and entry.get("algorithmic_bytes"):
         roofline["algorithmic_bytes"] = int(
             entry["algorithmic_bytes"] * nsub_max / ns_total)
@@ -739,7 +834,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak" if args.mode == "replicated" else "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 phase/accumulate, f16x2-split MFMA operands",
         "data": "synthetic (reference generators app/common/init.cpp, srand(0))",
         "config": {
             "workload": (f"{args.workload}: NR_STATIONS={w['nr_stations']} "

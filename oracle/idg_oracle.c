@@ -280,6 +280,214 @@ void oracle_degridder(int nr_subgrids, int grid_size, int subgrid_size,
   (void)nthreads;
 }
 
+/* ---- exact-accumulation twins (a measuring instrument; no reference
+ * counterpart).  The reference's phase, formed and rounded to f32 exactly
+ * as above, then cos/sin of that f32 value, every product and sum, the
+ * A-term and the taper in double: the value the reference's sequential f32
+ * sums approximate.  tests/test_gpu.py splits an output's error into the
+ * reference's own accumulation error and the candidate's with it (the
+ * reference metric grows with sqrt(|output|)). */
+typedef struct {
+  double re, im;
+} cd;
+
+static inline cd cdmul(cd a, cd b) {
+  cd r = {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+  return r;
+}
+
+static inline cd cdof(cf a) {
+  cd r = {(double)a.re, (double)a.im};
+  return r;
+}
+
+static void jones_mul_d(const cd *a, const cd *b, cd *c) {
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++) {
+      const cd x = cdmul(a[2 * i], b[j]), y = cdmul(a[2 * i + 1], b[2 + j]);
+      c[2 * i + j].re = x.re + y.re;
+      c[2 * i + j].im = x.im + y.im;
+    }
+}
+
+static void jones_herm_d(const cd *a, cd *b) {
+  b[0].re = a[0].re; b[0].im = -a[0].im;
+  b[1].re = a[2].re; b[1].im = -a[2].im;
+  b[2].re = a[1].re; b[2].im = -a[1].im;
+  b[3].re = a[3].re; b[3].im = -a[3].im;
+}
+
+static void gridder_exact_row(int s, int y, int grid_size, int S,
+                              float image_size, float w_step_in_lambda,
+                              int nr_channels, int nr_stations,
+                              const float *uvw,
+                              const float *wavenumbers, const cf *vis,
+                              const float *spheroidal, const float *aterms,
+                              const oracle_metadata *metadata, cd *out) {
+  const sg_setup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                   w_step_in_lambda);
+  for (int x = 0; x < S; x++) {
+    cd pix[NCORR];
+    memset(pix, 0, sizeof(pix));
+    const float l = lm_of(x, S, image_size);
+    const float m = lm_of(y, S, image_size);
+    const float n = n_of(l, m);
+    const float phase_offset =
+        fmaf(g.w_offset, n, fmaf(g.u_offset, l, g.v_offset * m));
+    for (int t = 0; t < g.nr_timesteps; t++) {
+      const size_t row = (size_t)g.time_offset + t;
+      const float u = uvw[3 * row + 0];
+      const float v = uvw[3 * row + 1];
+      const float w = uvw[3 * row + 2];
+      const float phase_index = fmaf(w, n, fmaf(u, l, v * m));
+      for (int c = 0; c < nr_channels; c++) {
+        const double phase =
+            (double)fmaf(-phase_index, wavenumbers[c], phase_offset);
+        const cd phasor = {cos(phase), sin(phase)};
+        const cf *v4 = vis + (row * nr_channels + c) * NCORR;
+        for (int p = 0; p < NCORR; p++) {
+          const cd q = cdmul(cdof(v4[p]), phasor);
+          pix[p].re += q.re;
+          pix[p].im += q.im;
+        }
+      }
+    }
+    cd a1[4], a2[4], a1h[4], tmp[4];
+    const cf *f1 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                            g.station1, y, x);
+    const cf *f2 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                            g.station2, y, x);
+    for (int i = 0; i < 4; i++) {
+      a1[i] = cdof(f1[i]);
+      a2[i] = cdof(f2[i]);
+    }
+    jones_herm_d(a1, a1h);
+    jones_mul_d(a1h, pix, tmp);
+    jones_mul_d(tmp, a2, pix);
+    const double sph = spheroidal[y * S + x];
+    for (int p = 0; p < NCORR; p++) {
+      cd *dst = out + (((size_t)s * NCORR + p) * S + y) * S + x;
+      dst->re = pix[p].re * sph;
+      dst->im = pix[p].im * sph;
+    }
+  }
+}
+
+void oracle_gridder_exact(int nr_subgrids, int grid_size, int subgrid_size,
+                          float image_size, float w_step_in_lambda,
+                          int nr_channels, int nr_stations, const float *uvw,
+                          const float *wavenumbers, const float *visibilities,
+                          const float *spheroidal, const float *aterms,
+                          const oracle_metadata *metadata, double *subgrids,
+                          int nthreads) {
+  if (nr_subgrids <= 0) return;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+  /* one (subgrid, row) per work item: a single large subgrid spreads too */
+  for (int sy = 0; sy < nr_subgrids * subgrid_size; sy++)
+    gridder_exact_row(sy / subgrid_size, sy % subgrid_size, grid_size,
+                      subgrid_size, image_size, w_step_in_lambda, nr_channels,
+                      nr_stations, uvw, wavenumbers, (const cf *)visibilities,
+                      spheroidal, aterms, metadata, (cd *)subgrids);
+  (void)nthreads;
+}
+
+static void degridder_exact_one(int s, int grid_size, int S,
+                                float image_size, float w_step_in_lambda,
+                                int nr_channels, int nr_stations,
+                                const float *uvw, const float *wavenumbers,
+                                cd *vis, const float *spheroidal,
+                                const float *aterms,
+                                const oracle_metadata *metadata,
+                                const cf *subgrids, cd *pixels) {
+  const sg_setup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                   w_step_in_lambda);
+  for (int y = 0; y < S; y++) {
+    for (int x = 0; x < S; x++) {
+      const double sph = spheroidal[y * S + x];
+      cd p[4], tmp[4], a1[4], a2[4], a2h[4];
+      for (int c = 0; c < NCORR; c++) {
+        const cf v = subgrids[(((size_t)s * NCORR + c) * S + y) * S + x];
+        p[c].re = sph * v.re;
+        p[c].im = sph * v.im;
+      }
+      const cf *f1 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station1, y, x);
+      const cf *f2 = aterm_at(aterms, nr_stations, S, g.aterm_index,
+                              g.station2, y, x);
+      for (int i = 0; i < 4; i++) {
+        a1[i] = cdof(f1[i]);
+        a2[i] = cdof(f2[i]);
+      }
+      jones_mul_d(a1, p, tmp);
+      jones_herm_d(a2, a2h);
+      jones_mul_d(tmp, a2h, pixels + ((size_t)y * S + x) * NCORR);
+    }
+  }
+  for (int t = 0; t < g.nr_timesteps; t++) {
+    const size_t row = (size_t)g.time_offset + t;
+    const float u = uvw[3 * row + 0];
+    const float v = uvw[3 * row + 1];
+    const float w = uvw[3 * row + 2];
+    for (int c = 0; c < nr_channels; c++) {
+      cd sum[NCORR];
+      memset(sum, 0, sizeof(sum));
+      const float k = wavenumbers[c];
+      for (int y = 0; y < S; y++) {
+        for (int x = 0; x < S; x++) {
+          const float l = lm_of(x, S, image_size);
+          const float m = lm_of(y, S, image_size);
+          const float n = n_of(l, m);
+          const float phase_index = fmaf(u, l, v * m) + w * n;
+          const float phase_offset =
+              fmaf(g.u_offset, l, g.v_offset * m) + g.w_offset * n;
+          const double phase = (double)fmaf(phase_index, k, -phase_offset);
+          const cd phasor = {cos(phase), sin(phase)};
+          const cd *px = pixels + ((size_t)y * S + x) * NCORR;
+          for (int p = 0; p < NCORR; p++) {
+            const cd q = cdmul(px[p], phasor);
+            sum[p].re += q.re;
+            sum[p].im += q.im;
+          }
+        }
+      }
+      cd *dst = vis + (row * nr_channels + c) * NCORR;
+      for (int p = 0; p < NCORR; p++) dst[p] = sum[p];
+    }
+  }
+}
+
+void oracle_degridder_exact(int nr_subgrids, int grid_size, int subgrid_size,
+                            float image_size, float w_step_in_lambda,
+                            int nr_channels, int nr_stations,
+                            const float *uvw, const float *wavenumbers,
+                            double *visibilities, const float *spheroidal,
+                            const float *aterms,
+                            const oracle_metadata *metadata,
+                            const float *subgrids, int nthreads) {
+  if (nr_subgrids <= 0) return;
+  const size_t scratch = (size_t)subgrid_size * subgrid_size * NCORR;
+#ifdef _OPENMP
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+  {
+    cd *pixels = (cd *)malloc(scratch * sizeof(cd));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int s = 0; s < nr_subgrids; s++)
+      degridder_exact_one(s, grid_size, subgrid_size, image_size,
+                          w_step_in_lambda, nr_channels, nr_stations, uvw,
+                          wavenumbers, (cd *)visibilities, spheroidal, aterms,
+                          metadata, (const cf *)subgrids, pixels);
+    free(pixels);
+  }
+  (void)nthreads;
+}
+
 double oracle_check_error(int64_t n, const float *A, const float *B,
                           int64_t *nnz_out) {
   float r_max = 1.0f, i_max = 1.0f;

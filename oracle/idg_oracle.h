@@ -60,6 +60,29 @@ void oracle_degridder(int nr_subgrids, int grid_size, int subgrid_size,
                       int nthreads);
 
 /*
+ * Exact-accumulation twins of the two kernels (a measuring instrument, no
+ * reference counterpart): the reference's f32 phase exactly as above, then
+ * cos/sin of it and every product, sum, A-term and taper in double.
+ * Outputs are double [re, im] pairs with the layouts above.
+ */
+void oracle_gridder_exact(int nr_subgrids, int grid_size, int subgrid_size,
+                          float image_size, float w_step_in_lambda,
+                          int nr_channels, int nr_stations, const float *uvw,
+                          const float *wavenumbers, const float *visibilities,
+                          const float *spheroidal, const float *aterms,
+                          const oracle_metadata *metadata, double *subgrids,
+                          int nthreads);
+
+void oracle_degridder_exact(int nr_subgrids, int grid_size, int subgrid_size,
+                            float image_size, float w_step_in_lambda,
+                            int nr_channels, int nr_stations,
+                            const float *uvw, const float *wavenumbers,
+                            double *visibilities, const float *spheroidal,
+                            const float *aterms,
+                            const oracle_metadata *metadata,
+                            const float *subgrids, int nthreads);
+
+/*
  * check_error metric of tests/test_util.hpp:28-92: A = candidate, B =
  * reference, n complex values.  Returns the normalised RMS error; PASS iff
  * <= 1e-5.  *nnz receives the number of entries with |B| > 0.

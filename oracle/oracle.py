@@ -54,7 +54,9 @@ class Oracle:
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run make -C oracle")
         self.lib = ctypes.CDLL(path)
-        for fn in (self.lib.oracle_gridder, self.lib.oracle_degridder):
+        for fn in (self.lib.oracle_gridder, self.lib.oracle_degridder,
+                   self.lib.oracle_gridder_exact,
+                   self.lib.oracle_degridder_exact):
             fn.argtypes = _KERNEL_ARGS + [_I]
             fn.restype = None
         self.lib.oracle_check_error.argtypes = [ctypes.c_int64, _P, _P, _P]
@@ -84,6 +86,35 @@ class Oracle:
                                   _ptr(visibilities), _ptr(spheroidal),
                                   _ptr(aterms), _ptr(md), _ptr(subgrids),
                                   nthreads)
+        return visibilities
+
+    def gridder_exact(self, nr_subgrids, grid_size, subgrid_size, image_size,
+                      w_step, nr_channels, nr_stations, uvw, wavenumbers,
+                      visibilities, spheroidal, aterms, metadata, subgrids,
+                      nthreads=1):
+        """The reference's f32 phases, everything after them in double
+        (oracle_gridder_exact); subgrids: float64 [..., 2]."""
+        assert subgrids.dtype == np.float64
+        md = _md(metadata)
+        self.lib.oracle_gridder_exact(
+            nr_subgrids, grid_size, subgrid_size, image_size, w_step,
+            nr_channels, nr_stations, _ptr(uvw), _ptr(wavenumbers),
+            _ptr(visibilities), _ptr(spheroidal), _ptr(aterms), _ptr(md),
+            _ptr(subgrids), nthreads)
+        return subgrids
+
+    def degridder_exact(self, nr_subgrids, grid_size, subgrid_size,
+                        image_size, w_step, nr_channels, nr_stations, uvw,
+                        wavenumbers, visibilities, spheroidal, aterms,
+                        metadata, subgrids, nthreads=1):
+        """As degridder, accumulated in double; visibilities: float64."""
+        assert visibilities.dtype == np.float64
+        md = _md(metadata)
+        self.lib.oracle_degridder_exact(
+            nr_subgrids, grid_size, subgrid_size, image_size, w_step,
+            nr_channels, nr_stations, _ptr(uvw), _ptr(wavenumbers),
+            _ptr(visibilities), _ptr(spheroidal), _ptr(aterms), _ptr(md),
+            _ptr(subgrids), nthreads)
         return visibilities
 
     def check_error(self, candidate, reference):

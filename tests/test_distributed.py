@@ -272,3 +272,48 @@ def test_gloo_world2_warmup_count_agreed(tmp_path):
     got = [np.load(str(tmp_path / f"r{r}.npy")) for r in range(2)]
     assert got[0][0] == 501 and got[1][0] == 334
     assert got[0][1] == got[1][1] == 501
+
+
+@pytest.mark.parametrize("n,counts", [(2, [1225, 1225]),
+                                      (4, [613, 612, 613, 612])])
+def test_bench_plain_command_launches_its_own_ranks(n, counts):
+    """`python bench.py --gpus N` without torchrun: the process
+    starts torch.distributed.run on itself as a child, the ranks rendezvous
+    on 127.0.0.1 and shard the batch, and rank 0's line is the command's
+    output.  --plan-only stops after the plan (no device on this host)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(ORACLE)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["IDG_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"),
+                        "--gpus", str(n), "--timeslots", "2", "--plan-only"],
+                       env=env, capture_output=True, text=True, timeout=300,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines()
+             if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == n and line["ranks_in_collective"] == n
+    assert line["config"]["nr_subgrids_per_gpu"] == counts
+    assert sum(counts) == line["config"]["nr_subgrids"] == 2450
+
+
+def test_bench_plain_command_propagates_a_rank_failure():
+    # a batch the generator rejects (negative timeslots) fails inside every
+    # rank, after the launch: the launcher's exit code must say so
+    import subprocess
+    import sys
+    repo = os.path.dirname(ORACLE)
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    env["IDG_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"),
+                        "--gpus", "2", "--timeslots", "-1", "--plan-only"],
+                       env=env, capture_output=True, text=True, timeout=300,
+                       cwd="/tmp")
+    assert r.returncode != 0
+    assert "torch.distributed" in r.stderr or "Error" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

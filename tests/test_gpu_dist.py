@@ -1,6 +1,7 @@
 """bench.py's multi-GPU path on the HIP kernels (run on the GPU box: -m gpu).
 
-`bench.py --gpus 2` under torchrun, with IDG_DIST_BACKEND=gloo so that both
+`bench.py --gpus 2` (as a plain command, and under torchrun), with
+IDG_DIST_BACKEND=gloo so that both
 ranks can share the box's one device (RCCL refuses two ranks on one GPU),
 shards BASELINE configs[1]'s subgrids over the ranks exactly as the 8-GPU run
 does (BASELINE configs[3]).  Its gathered gridder subgrids and degridded
@@ -39,17 +40,25 @@ def _run(cmd, env, timeout=240):
 
 
 @pytest.mark.timeout(600)
-def test_bench_two_ranks_sharded_equals_one_rank(tmp_path):
+@pytest.mark.parametrize("launcher", ["plain", "torchrun"])
+def test_bench_two_ranks_sharded_equals_one_rank(tmp_path, launcher):
+    """launcher "plain": `python bench.py --gpus 2` with no WORLD_SIZE starts
+    its own ranks (bench.launch_ranks); "torchrun": the driver's form."""
     common = ["--steps", "2", "--warmup", "1", "--timeslots", "2",
               "--no-cpu-baseline", "--no-weak"]
-    env = dict(os.environ)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     one = _run([sys.executable, "bench.py", "--gpus", "1", "--dump",
                 str(tmp_path / "one")] + common, env)
     env2 = dict(env, IDG_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                "--master-port", str(_port()), "bench.py", "--gpus", "2",
-                "--dump", str(tmp_path / "two")] + common, env2)
+    if launcher == "plain":
+        cmd = [sys.executable, "bench.py"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+               "--master-port", str(_port()), "bench.py"]
+    two = _run(cmd + ["--gpus", "2", "--dump", str(tmp_path / "two")] +
+               common, env2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["scaling"] == "strong"
     assert two["config"]["nr_subgrids_per_gpu"] == [1225, 1225]

@@ -125,3 +125,83 @@ def test_reference_builds_agree_bitwise():
                 a["wavenumbers"], a["visibilities"], a["spheroidal"],
                 a["aterms"], a["metadata"], g)
     assert np.array_equal(g, a["gridder_out"])
+
+
+# --------------------------------------------------------------------------
+# The exact-accumulation twins (oracle_*_exact): the instrument of the
+# large-T x C error split (tests/accuracy.py, tests/test_gpu_accuracy.py)
+# --------------------------------------------------------------------------
+def _exact(o, p, a):
+    ns, G, S = p["nr_subgrids"], p["grid_size"], p["subgrid_size"]
+    C, st = p["nr_channels"], p["nr_stations"]
+    img, ws = p["image_size"], p["w_step_in_lambda"]
+    g = np.zeros(a["gridder_out"].shape, np.float64)
+    o.gridder_exact(ns, G, S, img, ws, C, st, a["uvw"], a["wavenumbers"],
+                    a["visibilities"], a["spheroidal"], a["aterms"],
+                    a["metadata"], g, nthreads=4)
+    d = np.zeros(a["degridder_out"].shape, np.float64)
+    o.degridder_exact(ns, G, S, img, ws, C, st, a["uvw"], a["wavenumbers"],
+                      d, a["spheroidal"], a["aterms"], a["metadata"],
+                      a["subgrids"], nthreads=4)
+    return g, d
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_exact_twins_agree_with_reference_golden(oracle_lib, case):
+    # at golden sizes (T x C <= 4,096) the reference's f32 sums are within
+    # a few 1e-6 of the exact accumulation of its own phases
+    p, a = load_case(case)
+    g, d = _exact(oracle_lib, p, a)
+    assert oracle_lib.check_error(a["gridder_out"], g.astype(np.float32))[0] \
+        <= 5e-6
+    assert oracle_lib.check_error(a["degridder_out"],
+                                  d.astype(np.float32))[0] <= 5e-6
+
+
+def test_exact_gridder_matches_numpy_fp64_restatement(oracle_lib):
+    # an independent numpy restatement (tests/debug/grid_fp64.py: the same f32
+    # phase rounding, float64 everything else) of one subgrid
+    import importlib.util
+    import idg_amd
+    spec = importlib.util.spec_from_file_location(
+        "grid_fp64", os.path.join(os.path.dirname(__file__), "debug",
+                                  "grid_fp64.py"))
+    gf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gf)
+    st, ts, T, C, G, S = 2, 1, 8, 4, 1024, 32
+    a = idg_amd.generate(st, ts, T, C, G, S, nthreads=2)
+    g = np.zeros((1, 4, S, S, 2), np.float64)
+    oracle_lib.gridder_exact(1, G, S, idg_amd.IMAGE_SIZE, 0.0, C, st,
+                             a["uvw"], a["wavenumbers"], a["visibilities"],
+                             a["spheroidal"], a["aterms"], a["metadata"][:1],
+                             g)
+    ref = gf.grid_fp64(a, 0, G, S, C)
+    got = g[0, ..., 0] + 1j * g[0, ..., 1]
+    assert np.abs(got - ref).max() <= 1e-9 * np.abs(ref).max()
+
+
+@pytest.mark.skipif(not orc.Reference.available(portable=True),
+                    reason="oracle/_ref not built (needs /root/reference)")
+def test_reference_itself_misses_the_bar_at_large_TxC(oracle_lib):
+    """The fact behind the stated configs[2] deviation: at
+    T x C = 32,768 (-c with NR_CHANNELS=256, T = 128) the reference's own
+    CPU gridder output is more than 1e-5 from the exact sum of its own
+    phases in its own metric, while at the -c defaults it is ~1e-6."""
+    import idg_amd
+    ref = orc.Reference(portable=True)
+    errs = {}
+    for C in (16, 256):
+        a = idg_amd.generate(2, 2, 128, C, 1024, 32, nthreads=8)
+        ns = a["metadata"].size
+        args = (ns, 1024, 32, idg_amd.IMAGE_SIZE, 0.0, C, 2)
+        r = np.zeros((ns, 4, 32, 32, 2), np.float32)
+        ref.gridder(*args, a["uvw"], a["wavenumbers"], a["visibilities"],
+                    a["spheroidal"], a["aterms"], a["metadata"], r)
+        e = np.zeros(r.shape, np.float64)
+        oracle_lib.gridder_exact(*args, a["uvw"], a["wavenumbers"],
+                                 a["visibilities"], a["spheroidal"],
+                                 a["aterms"], a["metadata"], e,
+                                 nthreads=min(8, os.cpu_count() or 1))
+        errs[C] = oracle_lib.check_error(r, e.astype(np.float32))[0]
+    assert errs[16] < 2e-6, errs
+    assert errs[256] > TOLERANCE, errs
