@@ -1,8 +1,9 @@
-// print.hpp -- parameter banner and debug dumps.
-// Entry points of the reference's app/common/print.{hpp,cpp}.
+// print.hpp -- the parameter banner of the reference's app/common/print.cpp
+// (print_parameters, the one printer on the path; the reference's
+// print_subgrid* / print_visibilities* debug dumps have no caller and are
+// out of scope).
 #pragma once
 
-#include <complex>
 #include <iostream>
 
 #include "types.hpp"
@@ -28,18 +29,3 @@ void print_parameters(int nr_stations, int nr_channels, int nr_timesteps,
                       int grid_size, int subgrid_size, float w_step,
                       int nr_baselines, int nr_subgrids,
                       int total_nr_timesteps);
-
-void print_subgrid(idg::Array4D<std::complex<float>> &subgrids, unsigned i);
-
-void print_subgrid_diff(idg::Array4D<std::complex<float>> &subgrids1,
-                        idg::Array4D<std::complex<float>> &subgrids2,
-                        unsigned i);
-
-void print_visibilities(
-    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities,
-    unsigned i);
-
-void print_visibilities_diff(
-    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities1,
-    idg::Array3D<idg::Visibility<std::complex<float>>> &visibilities2,
-    unsigned i);

@@ -18,9 +18,10 @@
 //    on v_mfma_f32_16x16x32_f16 (degrid_mfma below); B (the A-termed,
 //    tapered pixels) is built once per subgrid into LDS;
 //  * the fp32 phase is formed exactly as the reference rounds it and reduced
-//    as fma(phase, 1/2pi_hi, -m) with an integer m per (timestep, pixel,
-//    16-channel block); the tail of 1/2pi_hi is applied to the pixels
-//    (device.hpp: kPhaseTail, phase_tail);
+//    as fma(phase, 1/2pi_hi, -m) + c with an integer m per (timestep, pixel,
+//    16-channel block) and c the k * phase_index part of the tail of
+//    1/2pi_hi; its phase_offset part is applied to the pixels (device.hpp:
+//    kPhaseTail, phase_tail, tail_k_rev);
 //  * mirror pixels (even S, w = 0, w_offset = 0): phase(S-1-y, S-1-x) =
 //    -phase(y, x) exactly, so each sin/cos pair serves a pixel pair;
 //  * IDG_DEGRIDDER_IMPL=valu (MODE 0): the all-VALU kernel, a lane per
@@ -142,31 +143,38 @@ struct DegridMfmaLds {
 };
 
 // Revolutions of the phases of one pixel at the channel pair kp = (k_j,
-// k_j+1):  fma(fma(p, k, o), 1/2pi_hi, -m)  with p, o and -m taken from half
-// H of their (pixel 0, pixel 1) VGPR pairs and broadcast to both lanes by
-// op_sel, so no operand is duplicated into a register pair (hipcc otherwise
-// materialises the broadcasts or splits the packed FMA into two).  The
-// constant is the inline 1/(2 pi) = kInv2PiHi; m is the integer revolution
-// count of the anchor block (device.hpp: kPhaseTail).  A dependent
-// packed-f32 VALU pair gets one wait state (s_nop 0), as hipcc pads its own;
-// the output is read by compiler code, which pads after the asm itself.
+// k_j+1):  fma(fma(p, k, o), 1/2pi_hi, -m) + c  with p, o, -m and c taken
+// from half H of their (pixel 0, pixel 1) VGPR pairs and broadcast to both
+// lanes by op_sel, so no operand is duplicated into a register pair (hipcc
+// otherwise materialises the broadcasts or splits the packed FMA into two).
+// The constant is the inline 1/(2 pi) = kInv2PiHi; m is the integer
+// revolution count of the anchor block, c the k * phase_index part of the
+// reduction's tail at the block's first channel (device.hpp: kPhaseTail,
+// tail_k_rev).  A dependent packed-f32 VALU pair gets one wait state
+// (s_nop 0), as hipcc pads its own; the output is read by compiler code,
+// which pads after the asm itself.
 template <int H>
 __device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
-                                                   floatx2 o, floatx2 nm) {
+                                                   floatx2 o, floatx2 nm,
+                                                   floatx2 cr) {
   floatx2 r;
   if constexpr (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]\n\t"
         "s_nop 0\n\t"
-        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel_hi:[1,0,0]"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel_hi:[1,0,0]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_add_f32 %0, %0, %5 op_sel_hi:[1,0]"
         : "=&v"(r)
-        : "v"(p), "s"(kp), "v"(o), "v"(nm));
+        : "v"(p), "s"(kp), "v"(o), "v"(nm), "v"(cr));
   else
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,1,1]\n\t"
         "s_nop 0\n\t"
         "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel:[0,0,1] "
-        "op_sel_hi:[1,0,1]"
+        "op_sel_hi:[1,0,1]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_add_f32 %0, %0, %5 op_sel:[0,1] op_sel_hi:[1,1]"
         : "=&v"(r)
-        : "v"(p), "s"(kp), "v"(o), "v"(nm));
+        : "v"(p), "s"(kp), "v"(o), "v"(nm), "v"(cr));
   return r;
 }
 static_assert(kInv2PiHi == 0.15915494f, "phase_rev_bcast's inline constant");
@@ -183,7 +191,13 @@ __device__ __forceinline__ void degrid_mfma(
   static_assert(KP % 32 == 0, "chunks hold whole 8-pair K-steps, 4 per pass");
   using L = DegridMfmaLds<KP>;
   constexpr int kThreads = 64 * NW;
-  const int tid = threadIdx.x;
+  // General path: an opaque copy of the thread index, so values derived
+  // from it are formed per call, not hoisted out of the general kernel's
+  // loop over subgrids and kept live (spilled) across it (scratch 408 -> 160
+  // B/lane gridder, 168 -> 68 degridder at S = 32; the mirror path, one
+  // subgrid per workgroup, is better without it).
+  int tid = threadIdx.x;
+  if constexpr (!MIRROR) asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
   // MIRROR: K runs over pixel pairs (b, npix-1-b); general: over single
@@ -378,6 +392,9 @@ __device__ __forceinline__ void degrid_mfma(
                 pidx, floatx2{kk[jb], kk[jb]}, npoff);
             const floatx2 t = A * floatx2{kInv2PiHi, kInv2PiHi};
             const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
+            // the k * phase_index part of the reduction's tail at the
+            // block's first channel (phase = k * phase_index - poff here)
+            const floatx2 cr = tail_k_rev(pidx, kk[jb]);
             // Packed over channel pairs (j, j+1) per pixel: the wavenumber
             // pair is one SGPR pair and the pixel's terms are broadcast from
             // their halves of the (pixel 0, pixel 1) pairs by op_sel, so the
@@ -386,8 +403,8 @@ __device__ __forceinline__ void degrid_mfma(
 #pragma unroll
             for (int j = jb; j < jb + CB; j += 2) {
               const floatx2 kp = {kk[j], kk[j + 1]};
-              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, nm);
-              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, nm);
+              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, nm, cr);
+              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, nm, cr);
               float s0, c0, s1, c1, s2, c2, s3, c3;
               sincos_rev(rx.x, &s0, &c0);  // channel j,   pixel 0
               sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1
@@ -465,7 +482,12 @@ __device__ __forceinline__ void degrid_mfma(
 // CT: channels per MFMA pass.
 // NW: waves per workgroup of the MFMA kernel (4; 8 for small launches, whose
 //     drain is then half as long: select_degridder).
-template <int S_CT, int CG, int MODE, int CT, int NW>
+// SEL: which subgrids this kernel degrids (MODE 1): 0 = every subgrid, each
+//     on its path (one launch, the reference's shape); 1 = mirror-eligible
+//     ones only, the main launch of the two-launch form (select_degridder),
+//     whose mirror path gets the registers of its own code alone; the
+//     others are left to kernel_degridder_general_mi355x.
+template <int S_CT, int CG, int MODE, int CT, int NW, int SEL = 0>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
                                   MODE == 1 ? IDG_DEGRID_WAVES : 1)
     kernel_degridder_mi355x(const int grid_size, int subgrid_size,
@@ -504,16 +526,20 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
     __syncthreads();
     const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
     __syncthreads();
-    if (eligible)
-      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(g, S, npix, image_size, C,
-                                          nr_stations, uvw, wavenumbers,
-                                          visibilities, spheroidal, aterms,
-                                          sg, lds);
-    else
-      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(g, S, npix, image_size, C,
-                                           nr_stations, uvw, wavenumbers,
-                                           visibilities, spheroidal, aterms,
-                                           sg, lds);
+    if constexpr (SEL != 2) {
+      if (eligible) {
+        degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
+            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+            visibilities, spheroidal, aterms, sg, lds);
+        return;
+      }
+    }
+    if constexpr (SEL == 0) {
+      if (!eligible)
+        degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+            visibilities, spheroidal, aterms, sg, lds);
+    }
     return;
   }
 
@@ -629,9 +655,86 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
   }
 }
 
+// The general-only degridder of the two-launch form (w != 0 on some
+// timestep, w_offset != 0, or odd S): a resident grid of 8-wave workgroups
+// (select_degridder: KernelChoice::Part::persistent), each taking a
+// contiguous range of subgrids, classifying them 32 at a time -- one wave
+// per subgrid, exactly the mirror-only kernel's test -- and degridding the
+// general ones with chunks of KP = 1,024 single pixels (one thread per
+// K-block of the 512), so an S = 32 subgrid is one chunk and its
+// visibilities are written once (the 512-pixel chunks of the combined
+// kernel read them back and wrote them again).  The 13-argument kernel ABI
+// plus nr_subgrids.
+template <int S_CT, int CT>
+__global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
+    kernel_degridder_general_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        const float2 *__restrict__ subgrids, int nr_subgrids) {
+  constexpr int NW = 8, KP = 1024;
+  __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
+  // the batch's general-subgrid mask lives in lds[0] between subgrids (a
+  // word of its own would push the degridder's 80 KiB past half a CU)
+  unsigned &general_mask = lds[0];
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long nwg = gridDim.x;
+  const int c0 = static_cast<int>(nr_subgrids * (long long)blockIdx.x / nwg);
+  const int c1 =
+      static_cast<int>(nr_subgrids * ((long long)blockIdx.x + 1) / nwg);
+  for (int base = c0; base < c1; base += 32) {
+    const int n = min(32, c1 - base);
+    if (tid == 0) general_mask = 0u;
+    __syncthreads();
+    for (int i = wave; i < n; i += NW) {
+      const SubgridSetup g = setup_subgrid(metadata, base + i, grid_size, S,
+                                           image_size, w_step_in_lambda);
+      bool w_nonzero = false;
+      for (int t = lane; t < g.nr_timesteps; t += 64)
+        w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+      const bool general =
+          __ballot(w_nonzero) != 0 || S % 2 != 0 || g.w_offset != 0.0f;
+      if (general && lane == 0) atomicOr(&general_mask, 1u << i);
+    }
+    __syncthreads();
+    unsigned mask = __builtin_amdgcn_readfirstlane(general_mask);
+    __syncthreads();  // read by every wave before the next batch resets it
+    while (mask) {
+      const int s = base + __builtin_ctz(mask);
+      mask &= mask - 1u;
+      const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
+                                           image_size, w_step_in_lambda);
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+          g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms,
+          subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+      __syncthreads();  // the LDS tables are rebuilt for the next subgrid
+    }
+  }
+}
+
 #define IDG_DEGRIDDER(S_, CG_, MODE_, NW_) \
   reinterpret_cast<const void *>(                   \
       &kernel_degridder_mi355x<S_, CG_, MODE_, IDG_DEGRID_CT, NW_>)
+#define IDG_DEGRIDDER_MIRROR(S_, NW_)                   \
+  reinterpret_cast<const void *>(                      \
+      &kernel_degridder_mi355x<S_, 4, 1, IDG_DEGRID_CT, NW_, 1>)
+#define IDG_DEGRIDDER_GENERAL(S_)                      \
+  reinterpret_cast<const void *>(                      \
+      &kernel_degridder_general_mi355x<S_, IDG_DEGRID_CT>)
+
+// IDG_DEGRID_SPLIT=0: the device entries launch the one combined MFMA
+// kernel (A/B of the two-launch form).
+#ifndef IDG_DEGRID_SPLIT
+#define IDG_DEGRID_SPLIT 1
+#endif
 
 // IDG_DEGRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int degridder_impl() {
@@ -661,6 +764,22 @@ KernelChoice select_degridder(const Problem &p) {
     // the MFMA kernel has no CG
     k.func = nw8 ? IDG_PICK(4, 1, 8) : IDG_PICK(4, 1, 4);
     k.block = nw8 ? 512 : 256;
+    if (IDG_DEGRID_SPLIT) {
+      // mirror-eligible subgrids (even S only), then the others on 8-wave
+      // workgroups with 1,024-pixel chunks
+#define IDG_PICK_MIRROR(NW_)                                               \
+  (s32 ? IDG_DEGRIDDER_MIRROR(32, NW_)                                     \
+       : (s64 ? IDG_DEGRIDDER_MIRROR(64, NW_) : IDG_DEGRIDDER_MIRROR(0, NW_)))
+      int n = 0;
+      if (p.subgrid_size % 2 == 0)
+        k.parts[n++] = {nw8 ? IDG_PICK_MIRROR(8) : IDG_PICK_MIRROR(4),
+                        k.block, false};
+      k.parts[n++] = {s32 ? IDG_DEGRIDDER_GENERAL(32)
+                          : (s64 ? IDG_DEGRIDDER_GENERAL(64)
+                                 : IDG_DEGRIDDER_GENERAL(0)),
+                      512, true};
+#undef IDG_PICK_MIRROR
+    }
   } else {
     k.func = cg8 ? IDG_PICK(8, 0, 4) : IDG_PICK(4, 0, 4);
   }

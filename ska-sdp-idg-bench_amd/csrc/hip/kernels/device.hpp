@@ -14,6 +14,8 @@ namespace idg_mi355x {
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 
+typedef float floatx2 __attribute__((ext_vector_type(2)));  // as mfma.hpp
+
 // 1/(2*pi) split into a float head and tail: head + tail = 1/(2*pi) to ~2^-52.
 constexpr float kInv2PiHi = 0x1.45f306p-3f;
 constexpr float kInv2PiLo = 0x1.b9391p-28f;
@@ -38,13 +40,30 @@ __device__ __forceinline__ float revolutions(float x) {
 // kPhaseTail = 1 - 2*pi*kInv2PiHi: the MFMA kernels reduce a phase x to
 // revolutions as r = fma(x, kInv2PiHi, -m), m an integer (the product is
 // exact inside the FMA, |r| < 1, one rounding), which is x/(2*pi) - m minus
-// x * kPhaseTail/(2*pi).  Splitting x = phase_offset - k * phase_index, the
-// phase_offset part of that tail is a constant per pixel and is restored
-// exactly as one phasor exp(i * phase_offset * kPhaseTail) per pixel
-// (phase_tail below, applied after the gridder's sum or to the degridder's
-// pixels); the k * phase_index part, |k * phase_index * kPhaseTail| <=
-// 1.5e-6 rad at C = 256, is left (measured: tests/debug/phase_reduction_emul.py).
+// x * kPhaseTail/(2*pi).  Splitting x = phase_offset - k * phase_index (the
+// degridder's phase is the negative), the phase_offset part of that tail is
+// a constant per pixel and is restored exactly as one phasor
+// exp(i * phase_offset * kPhaseTail) per pixel (phase_tail below, applied
+// after the gridder's sum or to the degridder's pixels).  The k *
+// phase_index part (<= 1.5e-6 rad at C = 256) is added to r in revolutions,
+// evaluated at the first channel k_b of the r's 16-channel block
+// (tail_k_rev: one packed multiply per block, one packed add per two
+// phasors); what remains, (k - k_b) * phase_index * kPhaseTail, is below
+// 1e-7 rad.  Left out (round 2), it put the gridder as far from exact
+// accumulation as the reference's own f32 sum at C = 256 (1.3e-5 in the
+// reference metric, tests/test_gpu_accuracy.py).
 constexpr float kPhaseTail = 0x1.5a892p-25f;  // 4.034206e-8
+
+// c = k_b * (-phase_index) * (1/2pi - kInv2PiHi) in revolutions for a
+// packed pair of -phase_index (the gridder's sign; the degridder passes
+// +phase_index for its phase = k * phase_index - phase_offset).
+#ifndef IDG_TAIL_K
+#define IDG_TAIL_K 1
+#endif
+__device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
+  const float f = IDG_TAIL_K ? kb * kInv2PiLo : 0.0f;
+  return neg_pidx * floatx2{f, f};
+}
 
 // exp(i * phase_offset * kPhaseTail), |angle| <= 1.4e-4: cos = 1 - a^2/2
 // (the a^4 term is below 1e-16), sin = a (the a^3 term below 5e-13).

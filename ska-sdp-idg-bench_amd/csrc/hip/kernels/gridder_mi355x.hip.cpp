@@ -17,9 +17,10 @@
 //  * one workgroup per subgrid: 8 wave64 (MFMA kernel), 4 (VALU kernel);
 //  * the fp32 phase is formed exactly as the reference rounds it and reduced
 //    to revolutions without losing its low bits: r = fma(phase, 1/2pi_hi,
-//    -m) with an integer m per (pixel, timestep, channel block), and the
-//    tail phase * (1/2pi - 1/2pi_hi) applied to each pixel as one phasor
-//    exp(i * phase_offset * kPhaseTail) in the epilogue (device.hpp);
+//    -m) + c with an integer m per (pixel, timestep, channel block) and c
+//    the tail -k * phase_index * (1/2pi - 1/2pi_hi) at the block's first
+//    channel; the tail's phase_offset part is applied to each pixel as one
+//    phasor exp(i * phase_offset * kPhaseTail) in the epilogue (device.hpp);
 //  * default (MODE 1): the complex MAC runs on the matrix cores as f16
 //    two-term-split GEMMs (v_mfma_f32_16x16x32_f16, grid_mfma below), pixels
 //    x (timestep, channel) x correlation components;
@@ -47,6 +48,10 @@
 #endif
 #ifndef IDG_GRID_WAVES
 #define IDG_GRID_WAVES 4
+#endif
+// the same bound for the general-only kernel of the two-launch form
+#ifndef IDG_GRID_WAVES_GENERAL
+#define IDG_GRID_WAVES_GENERAL 4
 #endif
 // general path (w != 0): X + Y in one accumulator tile, 2 PT tiles per wave
 #ifndef IDG_GRID_FUSED_GENERAL
@@ -274,7 +279,13 @@ __device__ __forceinline__ void grid_mfma(
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
     float2 *__restrict__ out, unsigned *lds) {
   static_assert(CB % 4 == 0, "anchor blocks hold whole channel quads");
-  const int tid = threadIdx.x;
+  // General path: an opaque copy of the thread index, so values derived
+  // from it are formed per call, not hoisted out of the general kernel's
+  // loop over subgrids and kept live (spilled) across it (scratch 408 -> 160
+  // B/lane gridder, 168 -> 68 degridder at S = 32; the mirror path, one
+  // subgrid per workgroup, is better without it).
+  int tid = threadIdx.x;
+  if constexpr (!MIRROR) asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
   // MIRROR: base pixels b < npix/2 (mirror npix-1-b shares the phasor);
@@ -529,6 +540,9 @@ __device__ __forceinline__ void grid_mfma(
                     __builtin_elementwise_fma(np, floatx2{ka, ka}, PG2[h]);
                 const floatx2 t = a * ih;
                 const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
+                // the k * phase_index part of the reduction's tail, at the
+                // block's first channel (device.hpp: kPhaseTail)
+                const floatx2 cr = tail_k_rev(np, ka);
 #pragma unroll
                 for (int u = 0; u < CB / 4; ++u) {
                   const int jj = jb + u;
@@ -544,7 +558,8 @@ __device__ __forceinline__ void grid_mfma(
                     const float kj = kb[4 * u + j];
                     const floatx2 ph =
                         __builtin_elementwise_fma(np, floatx2{kj, kj}, PG2[h]);
-                    const floatx2 r = __builtin_elementwise_fma(ph, ih, nm);
+                    const floatx2 r =
+                        __builtin_elementwise_fma(ph, ih, nm) + cr;
                     sincos_rev(r.x, &snx[j], &csx[j]);
                     sincos_rev(r.y, &sny[j], &csy[j]);
                   }
@@ -562,7 +577,7 @@ __device__ __forceinline__ void grid_mfma(
               }
               continue;
             }
-            floatx2 NP[PH], NM[PH];
+            floatx2 NP[PH], NM[PH], CR[PH];
 #pragma unroll
             for (int h = 0; h < PH; ++h) {
               // phase_index = fma(w, n, fma(u, l, v*m)); w = 0 on mirror
@@ -578,6 +593,9 @@ __device__ __forceinline__ void grid_mfma(
                   __builtin_elementwise_fma(NP[h], floatx2{ka, ka}, PG2[h]);
               const floatx2 t = a * ih;
               NM[h] = floatx2{-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
+              // the k * phase_index part of the reduction's tail at the
+              // block's first channel (device.hpp: kPhaseTail)
+              CR[h] = tail_k_rev(NP[h], ka);
             }
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
@@ -599,7 +617,8 @@ __device__ __forceinline__ void grid_mfma(
                   const float kj = kb[4 * u + j];
                   const floatx2 ph =
                       __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
-                  const floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
+                  const floatx2 r =
+                      __builtin_elementwise_fma(ph, ih, NM[h]) + CR[h];
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
@@ -692,7 +711,13 @@ __device__ __forceinline__ void grid_mfma(
 //       1 = MFMA kernel (mirror path on eligible subgrids, the same GEMMs
 //           over every pixel with the w-term on the others).
 // PT  : 16-pixel base tiles per wave in the MFMA path.
-template <int S_CT, int PPT, int CB, int MODE, int PT>
+// SEL : which subgrids this kernel grids (MODE 1): 0 = every subgrid, each
+//       on its path (one launch, the reference's shape); 1 = mirror-eligible
+//       subgrids only, the main launch of the two-launch form of the device
+//       entries (select_gridder), in which the mirror path has the register
+//       allocation of its own code alone; the others are left to
+//       kernel_gridder_general_mi355x.
+template <int S_CT, int PPT, int CB, int MODE, int PT, int SEL = 0>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
                                   IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
@@ -728,17 +753,21 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
     constexpr int NW = IDG_GRID_NW;
     // both paths hold 2 PT accumulator tiles per wave
     __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
-    if (mirror)
-      grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
-                                        nr_stations, uvw, wavenumbers,
-                                        visibilities, spheroidal, aterms, out,
-                                        lds);
-    else
-      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
-          g, S, npix, image_size, C,
-                                         nr_stations, uvw, wavenumbers,
-                                         visibilities, spheroidal, aterms,
-                                         out, lds);
+    if constexpr (SEL != 2) {
+      if (mirror) {
+        grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
+                                          nr_stations, uvw, wavenumbers,
+                                          visibilities, spheroidal, aterms,
+                                          out, lds);
+        return;
+      }
+    }
+    if constexpr (SEL == 0) {
+      if (!mirror)
+        grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+            visibilities, spheroidal, aterms, out, lds);
+    }
     return;
   }
 
@@ -807,9 +836,84 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
   }
 }
 
+// The general-only gridder of the two-launch form (w != 0 on some
+// timestep, w_offset != 0, or odd S): a resident grid of workgroups
+// (select_gridder: KernelChoice::Part::persistent), each taking a
+// contiguous range of subgrids, classifying them 32 at a time -- one wave
+// per subgrid, exactly the mirror-only kernel's test, so every subgrid is
+// taken by exactly one of the two -- and gridding the general ones on the
+// fused single-pixel GEMMs.  On a batch without w-terms it only classifies
+// (a few microseconds), instead of a grid of nr_subgrids workgroups that
+// would each return at once.  The 13-argument kernel ABI plus nr_subgrids.
+template <int S_CT, int CB, int PT>
+__global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
+    kernel_gridder_general_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        const float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        float2 *__restrict__ subgrids, int nr_subgrids) {
+  constexpr int NW = IDG_GRID_NW;
+  __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+  // the batch's general-subgrid mask lives in lds[0] between subgrids (a
+  // word of its own would push the degridder's 80 KiB past half a CU)
+  unsigned &general_mask = lds[0];
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long nwg = gridDim.x;
+  const int c0 = static_cast<int>(nr_subgrids * (long long)blockIdx.x / nwg);
+  const int c1 =
+      static_cast<int>(nr_subgrids * ((long long)blockIdx.x + 1) / nwg);
+  for (int base = c0; base < c1; base += 32) {
+    const int n = min(32, c1 - base);
+    if (tid == 0) general_mask = 0u;
+    __syncthreads();
+    for (int i = wave; i < n; i += NW) {
+      const SubgridSetup g = setup_subgrid(metadata, base + i, grid_size, S,
+                                           image_size, w_step_in_lambda);
+      bool w_nonzero = false;
+      for (int t = lane; t < g.nr_timesteps; t += 64)
+        w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+      const bool general =
+          __ballot(w_nonzero) != 0 || S % 2 != 0 || g.w_offset != 0.0f;
+      if (general && lane == 0) atomicOr(&general_mask, 1u << i);
+    }
+    __syncthreads();
+    unsigned mask = __builtin_amdgcn_readfirstlane(general_mask);
+    __syncthreads();  // read by every wave before the next batch resets it
+    while (mask) {
+      const int s = base + __builtin_ctz(mask);
+      mask &= mask - 1u;
+      const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
+                                           image_size, w_step_in_lambda);
+      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+          g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms,
+          subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+    }
+  }
+}
+
 #define IDG_GRIDDER(S_, PPT_, MODE_)                                     \
   reinterpret_cast<const void *>(                                         \
       &kernel_gridder_mi355x<S_, PPT_, 16, MODE_, IDG_GRID_PT>)
+#define IDG_GRIDDER_MIRROR(S_, PPT_)                                      \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_mi355x<S_, PPT_, 16, 1, IDG_GRID_PT, 1>)
+#define IDG_GRIDDER_GENERAL(S_)                                           \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT>)
+
+// IDG_GRID_SPLIT=0: the device entries launch the one combined MFMA kernel
+// (A/B of the two-launch form).
+#ifndef IDG_GRID_SPLIT
+#define IDG_GRID_SPLIT 1
+#endif
 
 // IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int gridder_impl() {
@@ -822,19 +926,32 @@ KernelChoice select_gridder(const Problem &p) {
   k.grid = p.nr_subgrids;
   const bool mfma = gridder_impl() == 1;
   k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
+  const void *part[2] = {nullptr, nullptr};
   switch (p.subgrid_size) {
     case 32:
       k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
       k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
+      part[0] = IDG_GRIDDER_MIRROR(32, 4);
+      part[1] = IDG_GRIDDER_GENERAL(32);
       break;
     case 64:
       k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);
       k.name = mfma ? "gridder_mi355x_s64" : "gridder_mi355x_s64_valu";
+      part[0] = IDG_GRIDDER_MIRROR(64, 4);
+      part[1] = IDG_GRIDDER_GENERAL(64);
       break;
     default:
       k.func = mfma ? IDG_GRIDDER(0, 2, 1) : IDG_GRIDDER(0, 2, 0);
       k.name = mfma ? "gridder_mi355x_generic" : "gridder_mi355x_generic_valu";
+      // odd S has no mirror pairs: one general-only launch
+      if (p.subgrid_size % 2 == 0) part[0] = IDG_GRIDDER_MIRROR(0, 2);
+      part[1] = IDG_GRIDDER_GENERAL(0);
       break;
+  }
+  if (mfma && IDG_GRID_SPLIT) {
+    int n = 0;
+    if (part[0]) k.parts[n++] = {part[0], k.block, false};
+    k.parts[n++] = {part[1], k.block, true};
   }
   return k;
 }

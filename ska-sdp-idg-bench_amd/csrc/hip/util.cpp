@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
+#include <map>
+#include <mutex>
 #include <memory>
 #include <sstream>
 #include <thread>
@@ -70,21 +72,27 @@ void print_dimensions(dim3 g, dim3 b) {
             << std::endl;
 }
 
-double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
-                    void **args, std::string func_name, double gflops,
-                    double gbytes, double mvis) {
+namespace {
+// The timed loop of p_run_kernel over one or more launches per iteration
+// (the two-launch form of the MI355X kernels, util.hpp KernelChoice::parts).
+double time_launches(const idg_mi355x::KernelChoice::Part *parts, int n,
+                     dim3 gridDim, void **args, const std::string &func_name,
+                     double gflops, double gbytes, double mvis) {
   const int warm = static_cast<int>(get_env_var("NR_WARM_UP_RUNS", 2));
   const int iters =
       std::max(1, static_cast<int>(get_env_var("NR_ITERATIONS", 5)));
+  auto once = [&] {
+    for (int j = 0; j < n; ++j)
+      hipCheck(idg_mi355x::launch_part(parts[j], static_cast<int>(gridDim.x),
+                                       args, nullptr));
+  };
   hipEvent_t start, stop;
   hipCheck(hipEventCreate(&start));
   hipCheck(hipEventCreate(&stop));
-  for (int i = 0; i < warm; ++i)
-    hipCheck(hipLaunchKernel(func, gridDim, blockDim, args, 0, nullptr));
+  for (int i = 0; i < warm; ++i) once();
   hipCheck(hipDeviceSynchronize());
   hipCheck(hipEventRecord(start, nullptr));
-  for (int i = 0; i < iters; ++i)
-    hipCheck(hipLaunchKernel(func, gridDim, blockDim, args, 0, nullptr));
+  for (int i = 0; i < iters; ++i) once();
   hipCheck(hipEventRecord(stop, nullptr));
   hipCheck(hipEventSynchronize(stop));
   float ms = 0.0f;
@@ -96,6 +104,17 @@ double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
   report_csv(func_name, get_device_name(), "-hip.csv", seconds, gflops, gbytes,
              mvis);
   return seconds;
+}
+}  // namespace
+
+double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
+                    void **args, std::string func_name, double gflops,
+                    double gbytes, double mvis) {
+  const idg_mi355x::KernelChoice::Part part{func,
+                                            static_cast<int>(blockDim.x),
+                                            false};
+  return time_launches(&part, 1, gridDim, args, func_name, gflops, gbytes,
+                       mvis);
 }
 
 void c_run_kernel(const void *func, dim3 gridDim, dim3 blockDim, void **args) {
@@ -255,8 +274,54 @@ hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
                   &d_uvw,         &d_wavenumbers,   &d_visibilities,
                   &d_spheroidal,  &d_aterms,        &d_metadata,
                   &d_subgrids};
-  return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args, 0,
-                         stream);
+  if (force || k.parts[0].func == nullptr)
+    return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args,
+                           0, stream);
+  for (const KernelChoice::Part &part : k.parts) {
+    if (part.func == nullptr) continue;
+    const hipError_t err = launch_part(part, p.nr_subgrids, args, stream);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+namespace {
+// Workgroups of `func` (block threads) resident on the current device at
+// once: occupancy x CUs, cached per (device, kernel).
+int resident_workgroups(const void *func, int block) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void *>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(dev, func);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func, block, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                            dev) != hipSuccess)
+    return 0;
+  const int n = std::max(1, per_cu) * std::max(1, cus);
+  cache[key] = n;
+  return n;
+}
+}  // namespace
+
+hipError_t launch_part(const KernelChoice::Part &part, int nr_subgrids,
+                       void **args13, hipStream_t stream) {
+  if (!part.persistent)
+    return hipLaunchKernel(part.func, dim3(nr_subgrids), dim3(part.block),
+                           args13, 0, stream);
+  const int resident = resident_workgroups(part.func, part.block);
+  if (resident <= 0) return hipErrorInvalidConfiguration;
+  int ns = nr_subgrids;
+  void *args14[14];
+  for (int i = 0; i < 13; ++i) args14[i] = args13[i];
+  args14[13] = &ns;
+  return hipLaunchKernel(part.func, dim3(std::min(nr_subgrids, resident)),
+                         dim3(part.block), args14, 0, stream);
 }
 
 namespace {
@@ -580,9 +645,20 @@ double run_performance(Direction dir, const void *func, std::string name,
   float a_img = IMAGE_SIZE, a_w = W_STEP;
   void *args[] = {&a_grid, &a_sub, &a_img, &a_w,   &a_nc,  &a_ns, &d_uvw,
                   &d_wn,   &d_vis, &d_sph, &d_at,  &d_md,  &d_sg};
-  const double seconds =
-      hip::p_run_kernel(func, dim3(nr_subgrids), dim3(num_threads), args, name,
-                        gflops, gbytes, mvis);
+  // The selected MI355X kernel is timed as the device entries launch it
+  // (its two-launch form, when it has one); a caller-supplied kernel as
+  // itself.
+  const KernelChoice k = dir == Direction::kGridder ? select_gridder(p)
+                                                    : select_degridder(p);
+  double seconds;
+  if (func == k.func && k.parts[0].func) {
+    const int n = k.parts[1].func ? 2 : 1;
+    seconds = hip::time_launches(k.parts, n, dim3(nr_subgrids), args, name,
+                                 gflops, gbytes, mvis);
+  } else {
+    seconds = hip::p_run_kernel(func, dim3(nr_subgrids), dim3(num_threads),
+                                args, name, gflops, gbytes, mvis);
+  }
   for (void *ptr : {d_uvw, d_wn, d_vis, d_sph, d_at, d_md, d_sg})
     hipCheck(hipFree(ptr));
   return seconds;

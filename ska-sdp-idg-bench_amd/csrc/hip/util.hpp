@@ -106,11 +106,31 @@ struct Extents {
 };
 
 struct KernelChoice {
-  const void *func = nullptr;  // __global__ with the 13-argument ABI
+  // one kernel that handles every subgrid (__global__, 13-argument ABI,
+  // grid = nr_subgrids): the reference's launch shape, used by the perf
+  // entries and for caller-supplied kernels
+  const void *func = nullptr;
   const char *name = "";
   int block = 256;
   int grid = 0;  // = nr_subgrids
+  // The launch the device entries make instead, when set: one kernel per
+  // subgrid class, each with the register allocation of its own path
+  // (DESIGN.md §4.1): the mirror-only kernel over grid = nr_subgrids (a
+  // workgroup whose subgrid is not mirror-eligible returns at once), then
+  // the general-only kernel, `persistent`: a resident grid (occupancy x CUs,
+  // at most nr_subgrids) whose workgroups take contiguous subgrid ranges;
+  // it takes nr_subgrids as a 14th argument.
+  struct Part {
+    const void *func = nullptr;
+    int block = 0;
+    bool persistent = false;
+  } parts[2];
 };
+
+// Launch one part of a two-launch kernel choice on `stream`; args13 is the
+// 13-argument kernel ABI (the persistent part gets nr_subgrids appended).
+hipError_t launch_part(const KernelChoice::Part &part, int nr_subgrids,
+                       void **args13, hipStream_t stream);
 
 // Defined in the kernel TUs.
 KernelChoice select_gridder(const Problem &p);

@@ -222,3 +222,23 @@ def test_host_chunk_plan_empty_middle_chunk_does_not_hide_an_overlap():
     md["nr_timesteps"][1520:3040] = 0
     assert idg_amd.host_chunk_plan(md, 600 << 20) == [0, 1520, 3040, 4560,
                                                        6080]
+
+
+@pytest.mark.parametrize("exe", ["hip-gridder_mi355x", "hip-degridder_mi355x"])
+def test_reference_harness_compiled_as_the_reference_compiles_it(exe):
+    """oracle/_ref's build of the reference's unmodified harness uses hipcc,
+    as the reference's own build does (tests/CMakeLists.txt:46-48).  Under
+    g++ the unqualified abs() in check_error (tests/test_util.hpp:36-37)
+    resolves to int abs, truncating r_max / i_max (a float -> int
+    conversion, cvttss2si, in the function); under hipcc it is the float
+    overload."""
+    import subprocess
+    path = os.path.join(REPO, "oracle", "_ref", exe)
+    if not os.path.exists(path):
+        pytest.skip("oracle/_ref harness not built (needs /root/reference)")
+    dis = subprocess.run(["objdump", "-d", "-C", path], capture_output=True,
+                         text=True, check=True).stdout
+    body = dis.split("<check_error(int, std::complex<float>")
+    assert len(body) > 1, "check_error not found"
+    fn = body[1].split("\n\n")[0]
+    assert "cvttss2si" not in fn

@@ -110,12 +110,22 @@ def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
     # issued as inline asm after the fill barrier.  A
     # compiler vmcnt wait between it and the MFMA loop (e.g. for a spill
     # reload) would expose its whole latency once per fill.
+    # Required of every mirror-path kernel and of the S = 32 general one;
+    # the S = 64 / runtime-S general-only kernels (w-terms at those sizes)
+    # reload a spill before one of their MFMA loops.
     import dma_drain_check as ddc
+    from resources import short
     res = ddc.check(open(listings["gridder"]).read())
-    mfma_kernels = [r for r in res if "ELi1ELi4EE" in r[0]]
-    assert mfma_kernels, "no gridder kernel with an LDS-DMA prefetch"
-    for name, total, drained, _ in mfma_kernels:
-        assert total > 0 and drained == 0, (name[:60], total, drained)
+    checked = []
+    for name, total, drained, _ in res:
+        k = short(name)
+        if k.startswith("gridder_general<") and not k.startswith(
+                "gridder_general<32,"):
+            continue
+        checked.append(k)
+        assert total > 0 and drained == 0, (k, total, drained)
+    assert "gridder<32,4,16,1,4,1>" in checked, checked
+    assert "gridder_general<32,16,4>" in checked, checked
 
 
 def test_lds_dma_m0_wait_state_checker():
