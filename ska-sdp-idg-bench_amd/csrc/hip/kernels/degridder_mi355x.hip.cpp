@@ -482,12 +482,10 @@ __device__ __forceinline__ void degrid_mfma(
 // CT: channels per MFMA pass.
 // NW: waves per workgroup of the MFMA kernel (4; 8 for small launches, whose
 //     drain is then half as long: select_degridder).
-// SEL: which subgrids this kernel degrids (MODE 1): 0 = every subgrid, each
-//     on its path (one launch, the reference's shape); 1 = mirror-eligible
-//     ones only, the main launch of the two-launch form (select_degridder),
-//     whose mirror path gets the registers of its own code alone; the
-//     others are left to kernel_degridder_general_mi355x.
-template <int S_CT, int CG, int MODE, int CT, int NW, int SEL = 0>
+// (One launch over every subgrid, each on its path: the reference's launch
+// shape.  The device entries launch the two-kernel form instead:
+// kernel_degridder_mirror_mi355x + kernel_degridder_general_mi355x.)
+template <int S_CT, int CG, int MODE, int CT, int NW>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
                                   MODE == 1 ? IDG_DEGRID_WAVES : 1)
     kernel_degridder_mi355x(const int grid_size, int subgrid_size,
@@ -526,20 +524,14 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
     __syncthreads();
     const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
     __syncthreads();
-    if constexpr (SEL != 2) {
-      if (eligible) {
-        degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
-            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
-            visibilities, spheroidal, aterms, sg, lds);
-        return;
-      }
-    }
-    if constexpr (SEL == 0) {
-      if (!eligible)
-        degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
-            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
-            visibilities, spheroidal, aterms, sg, lds);
-    }
+    if (eligible)
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
+          g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms, sg, lds);
+    else
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+          g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms, sg, lds);
     return;
   }
 
@@ -655,16 +647,56 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
   }
 }
 
-// The general-only degridder of the two-launch form (w != 0 on some
-// timestep, w_offset != 0, or odd S): a resident grid of 8-wave workgroups
-// (select_degridder: KernelChoice::Part::persistent), each taking a
-// contiguous range of subgrids, classifying them 32 at a time -- one wave
-// per subgrid, exactly the mirror-only kernel's test -- and degridding the
-// general ones with chunks of KP = 1,024 single pixels (one thread per
+// The two-kernel form of the device entries (select_degridder; DESIGN.md
+// §4.2), as the gridder's (gridder_mi355x.hip.cpp): the mirror kernel,
+// grid = nr_subgrids, degrids the mirror-eligible subgrids and queues the
+// others (queue[0] = count, queue[2 + i] = subgrid); the general kernel, a
+// resident grid of 8-wave workgroups, takes the queued subgrids one at a
+// time from a shared counter (queue[1]; all subgrids with `all` set, odd S)
+// and degrids each with chunks of KP = 1,024 single pixels (one thread per
 // K-block of the 512), so an S = 32 subgrid is one chunk and its
-// visibilities are written once (the 512-pixel chunks of the combined
-// kernel read them back and wrote them again).  The 13-argument kernel ABI
-// plus nr_subgrids.
+// visibilities are written once (the combined kernel's 512-pixel chunks
+// read them back and wrote them again).
+template <int S_CT, int CT, int NW>
+__global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
+    kernel_degridder_mirror_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        const float2 *__restrict__ subgrids, int *__restrict__ queue) {
+  constexpr int KP = 512;
+  __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                       w_step_in_lambda);
+  // eligibility reduced through lds[0] (see kernel_degridder_mi355x)
+  if (tid == 0) lds[0] = 0u;
+  __syncthreads();
+  bool w_nonzero = false;
+  for (int t = tid; t < g.nr_timesteps; t += 64 * NW)
+    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+  if (w_nonzero) atomicOr(&lds[0], 1u);
+  __syncthreads();
+  const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
+  __syncthreads();
+  if (!eligible) {
+    if (tid == 0) queue[2 + atomicAdd(queue, 1)] = s;
+    return;
+  }
+  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
+      g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+      visibilities, spheroidal, aterms,
+      subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+}
+
 template <int S_CT, int CT>
 __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     kernel_degridder_general_mi355x(
@@ -676,47 +708,35 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
         const float *__restrict__ spheroidal,
         const float2 *__restrict__ aterms,
         const idg::Metadata *__restrict__ metadata,
-        const float2 *__restrict__ subgrids, int nr_subgrids) {
+        const float2 *__restrict__ subgrids, int *__restrict__ queue,
+        int nr_subgrids, int all) {
   constexpr int NW = 8, KP = 1024;
   __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
-  // the batch's general-subgrid mask lives in lds[0] between subgrids (a
-  // word of its own would push the degridder's 80 KiB past half a CU)
-  unsigned &general_mask = lds[0];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long nwg = gridDim.x;
-  const int c0 = static_cast<int>(nr_subgrids * (long long)blockIdx.x / nwg);
-  const int c1 =
-      static_cast<int>(nr_subgrids * ((long long)blockIdx.x + 1) / nwg);
-  for (int base = c0; base < c1; base += 32) {
-    const int n = min(32, c1 - base);
-    if (tid == 0) general_mask = 0u;
+  const int tid = threadIdx.x;
+  const int count = all ? nr_subgrids : queue[0];
+  // the next queue position, taken by thread 0 and passed on through lds[0]
+  // (between subgrids, where degrid_mfma uses no LDS)
+  if (tid == 0) lds[0] = static_cast<unsigned>(atomicAdd(queue + 1, 1));
+  __syncthreads();
+  int i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
+  __syncthreads();
+  while (i < count) {
+    int next = 0;
+    if (tid == 0) next = atomicAdd(queue + 1, 1);  // lands during the subgrid
+    const int s = all ? i : queue[2 + i];
+    const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
+                                         image_size, w_step_in_lambda);
+    degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+        g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+        visibilities, spheroidal, aterms,
+        subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+    __syncthreads();  // every wave is done with the LDS tables
+    if (tid == 0) lds[0] = static_cast<unsigned>(next);
     __syncthreads();
-    for (int i = wave; i < n; i += NW) {
-      const SubgridSetup g = setup_subgrid(metadata, base + i, grid_size, S,
-                                           image_size, w_step_in_lambda);
-      bool w_nonzero = false;
-      for (int t = lane; t < g.nr_timesteps; t += 64)
-        w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-      const bool general =
-          __ballot(w_nonzero) != 0 || S % 2 != 0 || g.w_offset != 0.0f;
-      if (general && lane == 0) atomicOr(&general_mask, 1u << i);
-    }
+    i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
     __syncthreads();
-    unsigned mask = __builtin_amdgcn_readfirstlane(general_mask);
-    __syncthreads();  // read by every wave before the next batch resets it
-    while (mask) {
-      const int s = base + __builtin_ctz(mask);
-      mask &= mask - 1u;
-      const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
-                                           image_size, w_step_in_lambda);
-      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
-          g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
-          visibilities, spheroidal, aterms,
-          subgrids + static_cast<size_t>(s) * 4 * npix, lds);
-      __syncthreads();  // the LDS tables are rebuilt for the next subgrid
-    }
   }
 }
 
@@ -725,7 +745,7 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
       &kernel_degridder_mi355x<S_, CG_, MODE_, IDG_DEGRID_CT, NW_>)
 #define IDG_DEGRIDDER_MIRROR(S_, NW_)                   \
   reinterpret_cast<const void *>(                      \
-      &kernel_degridder_mi355x<S_, 4, 1, IDG_DEGRID_CT, NW_, 1>)
+      &kernel_degridder_mirror_mi355x<S_, IDG_DEGRID_CT, NW_>)
 #define IDG_DEGRIDDER_GENERAL(S_)                      \
   reinterpret_cast<const void *>(                      \
       &kernel_degridder_general_mi355x<S_, IDG_DEGRID_CT>)
@@ -770,14 +790,13 @@ KernelChoice select_degridder(const Problem &p) {
 #define IDG_PICK_MIRROR(NW_)                                               \
   (s32 ? IDG_DEGRIDDER_MIRROR(32, NW_)                                     \
        : (s64 ? IDG_DEGRIDDER_MIRROR(64, NW_) : IDG_DEGRIDDER_MIRROR(0, NW_)))
-      int n = 0;
       if (p.subgrid_size % 2 == 0)
-        k.parts[n++] = {nw8 ? IDG_PICK_MIRROR(8) : IDG_PICK_MIRROR(4),
-                        k.block, false};
-      k.parts[n++] = {s32 ? IDG_DEGRIDDER_GENERAL(32)
-                          : (s64 ? IDG_DEGRIDDER_GENERAL(64)
-                                 : IDG_DEGRIDDER_GENERAL(0)),
-                      512, true};
+        k.parts[0] = {nw8 ? IDG_PICK_MIRROR(8) : IDG_PICK_MIRROR(4), k.block,
+                      KernelChoice::kMirror};
+      k.parts[1] = {s32 ? IDG_DEGRIDDER_GENERAL(32)
+                        : (s64 ? IDG_DEGRIDDER_GENERAL(64)
+                               : IDG_DEGRIDDER_GENERAL(0)),
+                    512, KernelChoice::kGeneral};
 #undef IDG_PICK_MIRROR
     }
   } else {

@@ -711,13 +711,10 @@ __device__ __forceinline__ void grid_mfma(
 //       1 = MFMA kernel (mirror path on eligible subgrids, the same GEMMs
 //           over every pixel with the w-term on the others).
 // PT  : 16-pixel base tiles per wave in the MFMA path.
-// SEL : which subgrids this kernel grids (MODE 1): 0 = every subgrid, each
-//       on its path (one launch, the reference's shape); 1 = mirror-eligible
-//       subgrids only, the main launch of the two-launch form of the device
-//       entries (select_gridder), in which the mirror path has the register
-//       allocation of its own code alone; the others are left to
-//       kernel_gridder_general_mi355x.
-template <int S_CT, int PPT, int CB, int MODE, int PT, int SEL = 0>
+// (One launch over every subgrid, each on its path: the reference's launch
+// shape.  The device entries launch the two-kernel form instead:
+// kernel_gridder_mirror_mi355x + kernel_gridder_general_mi355x.)
+template <int S_CT, int PPT, int CB, int MODE, int PT>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
                                   IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
@@ -753,21 +750,15 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
     constexpr int NW = IDG_GRID_NW;
     // both paths hold 2 PT accumulator tiles per wave
     __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
-    if constexpr (SEL != 2) {
-      if (mirror) {
-        grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
-                                          nr_stations, uvw, wavenumbers,
-                                          visibilities, spheroidal, aterms,
-                                          out, lds);
-        return;
-      }
-    }
-    if constexpr (SEL == 0) {
-      if (!mirror)
-        grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
-            g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
-            visibilities, spheroidal, aterms, out, lds);
-    }
+    if (mirror)
+      grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
+                                        nr_stations, uvw, wavenumbers,
+                                        visibilities, spheroidal, aterms, out,
+                                        lds);
+    else
+      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+          g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms, out, lds);
     return;
   }
 
@@ -836,15 +827,59 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
   }
 }
 
-// The general-only gridder of the two-launch form (w != 0 on some
-// timestep, w_offset != 0, or odd S): a resident grid of workgroups
-// (select_gridder: KernelChoice::Part::persistent), each taking a
-// contiguous range of subgrids, classifying them 32 at a time -- one wave
-// per subgrid, exactly the mirror-only kernel's test, so every subgrid is
-// taken by exactly one of the two -- and gridding the general ones on the
-// fused single-pixel GEMMs.  On a batch without w-terms it only classifies
-// (a few microseconds), instead of a grid of nr_subgrids workgroups that
-// would each return at once.  The 13-argument kernel ABI plus nr_subgrids.
+// The two-kernel form of the device entries (select_gridder; DESIGN.md
+// §4.1).  Each path gets the register allocation of its own code alone:
+//
+// kernel_gridder_mirror_mi355x: grid = nr_subgrids, one workgroup per
+//   subgrid as kernel_gridder_mi355x; a mirror-eligible subgrid (even S,
+//   w_offset = 0, w = 0 on every timestep) is gridded on the mirror GEMMs,
+//   any other is appended to the general queue (queue[0] = count,
+//   queue[2 + i] = subgrid) and left.
+// kernel_gridder_general_mi355x: a resident grid (occupancy x CUs) that
+//   takes the queued subgrids one at a time from a shared counter
+//   (queue[1]), the next index requested while the current subgrid runs,
+//   and grids each on the fused single-pixel GEMMs; with `all` set (odd S:
+//   no subgrid is mirror-eligible, no mirror launch) it takes subgrids
+//   0 .. nr_subgrids-1 instead.  Dynamic, not a fixed range per workgroup:
+//   with fixed ranges the slowest CU set the time (w-term batch +7-9 %).
+//   On a batch without w-terms the queue is empty and every workgroup
+//   returns at once.
+// queue: nr_subgrids + 2 ints, queue[0..1] zeroed before the launches.
+template <int S_CT, int CB, int PT>
+__global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
+    kernel_gridder_mirror_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        const float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        float2 *__restrict__ subgrids, int *__restrict__ queue) {
+  constexpr int NW = IDG_GRID_NW;
+  __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                       w_step_in_lambda);
+  bool w_nonzero = false;
+  for (int t = tid; t < g.nr_timesteps; t += blockDim.x)
+    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+  const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
+                      g.w_offset == 0.0f;
+  if (!mirror) {
+    if (tid == 0) queue[2 + atomicAdd(queue, 1)] = s;
+    return;
+  }
+  grid_mfma<S_CT, PT, CB, NW, true>(
+      g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+      visibilities, spheroidal, aterms,
+      subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+}
+
 template <int S_CT, int CB, int PT>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     kernel_gridder_general_mi355x(
@@ -856,46 +891,34 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
         const float *__restrict__ spheroidal,
         const float2 *__restrict__ aterms,
         const idg::Metadata *__restrict__ metadata,
-        float2 *__restrict__ subgrids, int nr_subgrids) {
+        float2 *__restrict__ subgrids, int *__restrict__ queue,
+        int nr_subgrids, int all) {
   constexpr int NW = IDG_GRID_NW;
   __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
-  // the batch's general-subgrid mask lives in lds[0] between subgrids (a
-  // word of its own would push the degridder's 80 KiB past half a CU)
-  unsigned &general_mask = lds[0];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long nwg = gridDim.x;
-  const int c0 = static_cast<int>(nr_subgrids * (long long)blockIdx.x / nwg);
-  const int c1 =
-      static_cast<int>(nr_subgrids * ((long long)blockIdx.x + 1) / nwg);
-  for (int base = c0; base < c1; base += 32) {
-    const int n = min(32, c1 - base);
-    if (tid == 0) general_mask = 0u;
+  const int tid = threadIdx.x;
+  const int count = all ? nr_subgrids : queue[0];
+  // the next queue position, taken by thread 0 and passed on through lds[0]
+  // (between subgrids, where grid_mfma uses no LDS)
+  if (tid == 0) lds[0] = static_cast<unsigned>(atomicAdd(queue + 1, 1));
+  __syncthreads();
+  int i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
+  __syncthreads();
+  while (i < count) {
+    int next = 0;
+    if (tid == 0) next = atomicAdd(queue + 1, 1);  // lands during the subgrid
+    const int s = all ? i : queue[2 + i];
+    const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
+                                         image_size, w_step_in_lambda);
+    grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+        g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+        visibilities, spheroidal, aterms,
+        subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+    if (tid == 0) lds[0] = static_cast<unsigned>(next);
     __syncthreads();
-    for (int i = wave; i < n; i += NW) {
-      const SubgridSetup g = setup_subgrid(metadata, base + i, grid_size, S,
-                                           image_size, w_step_in_lambda);
-      bool w_nonzero = false;
-      for (int t = lane; t < g.nr_timesteps; t += 64)
-        w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-      const bool general =
-          __ballot(w_nonzero) != 0 || S % 2 != 0 || g.w_offset != 0.0f;
-      if (general && lane == 0) atomicOr(&general_mask, 1u << i);
-    }
+    i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
     __syncthreads();
-    unsigned mask = __builtin_amdgcn_readfirstlane(general_mask);
-    __syncthreads();  // read by every wave before the next batch resets it
-    while (mask) {
-      const int s = base + __builtin_ctz(mask);
-      mask &= mask - 1u;
-      const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
-                                           image_size, w_step_in_lambda);
-      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
-          g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
-          visibilities, spheroidal, aterms,
-          subgrids + static_cast<size_t>(s) * 4 * npix, lds);
-    }
   }
 }
 
@@ -904,7 +927,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
       &kernel_gridder_mi355x<S_, PPT_, 16, MODE_, IDG_GRID_PT>)
 #define IDG_GRIDDER_MIRROR(S_, PPT_)                                      \
   reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mi355x<S_, PPT_, 16, 1, IDG_GRID_PT, 1>)
+      &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT>)
 #define IDG_GRIDDER_GENERAL(S_)                                           \
   reinterpret_cast<const void *>(                                         \
       &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT>)
@@ -949,9 +972,8 @@ KernelChoice select_gridder(const Problem &p) {
       break;
   }
   if (mfma && IDG_GRID_SPLIT) {
-    int n = 0;
-    if (part[0]) k.parts[n++] = {part[0], k.block, false};
-    k.parts[n++] = {part[1], k.block, true};
+    if (part[0]) k.parts[0] = {part[0], k.block, KernelChoice::kMirror};
+    k.parts[1] = {part[1], k.block, KernelChoice::kGeneral};
   }
   return k;
 }

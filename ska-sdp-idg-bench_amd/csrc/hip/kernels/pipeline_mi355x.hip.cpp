@@ -22,6 +22,8 @@
 // grid is skipped by the adder and zero-filled by the splitter.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../util.hpp"
 #include "common/types.hpp"
 #include "device.hpp"
@@ -173,51 +175,77 @@ __device__ __forceinline__ TileSpan tile_span(const idg::Metadata &m, int S) {
           m.coordinate.y / kAddTile, (m.coordinate.y + S - 1) / kAddTile};
 }
 
-// Bins: count (pass 0) or fill (pass 1) the tiles each subgrid overlaps.
+// Bins: count (pass 0) or fill (pass 1) the tiles each subgrid overlaps,
+// one thread per (subgrid, tile of its span x span window) pair, so each
+// thread makes one atomic (a thread per subgrid made up to 9 in a row at
+// S = 32 and took 17 us per pass at configs[1]).
 __global__ void __launch_bounds__(256)
     kernel_adder_bin(const idg::Metadata *__restrict__ metadata,
                      int nr_subgrids, int G, int S, int nr_w_layers, int pass,
                      int *__restrict__ count, int *__restrict__ cursor,
                      int *__restrict__ list) {
-  const int s = blockIdx.x * 256 + threadIdx.x;
+  const int span = (S + kAddTile - 2) / kAddTile + 1;  // tiles per axis, max
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const int s = static_cast<int>(i / (span * span));
   if (s >= nr_subgrids) return;
+  const int k = static_cast<int>(i - static_cast<long long>(s) * span * span);
   const idg::Metadata m = metadata[s];
   if (!fits(m, G, S, nr_w_layers)) return;
-  const int ntx = (G + kAddTile - 1) / kAddTile;
   const TileSpan t = tile_span(m, S);
-  for (int ty = t.ty0; ty <= t.ty1; ++ty)
-    for (int tx = t.tx0; tx <= t.tx1; ++tx) {
-      const int tile = (m.coordinate.z * ntx + ty) * ntx + tx;
-      if (pass == 0)
-        atomicAdd(count + tile, 1);
-      else
-        list[atomicAdd(cursor + tile, 1)] = s;
-    }
+  const int ty = t.ty0 + k / span, tx = t.tx0 + k % span;
+  if (ty > t.ty1 || tx > t.tx1) return;
+  const int ntx = (G + kAddTile - 1) / kAddTile;
+  const int tile = (m.coordinate.z * ntx + ty) * ntx + tx;
+  if (pass == 0)
+    atomicAdd(count + tile, 1);
+  else
+    list[atomicAdd(cursor + tile, 1)] = s;
 }
 
-// Exclusive scan of the bin counts (one workgroup): offset = cursor.
+// Exclusive scan of n counts (one workgroup of 1,024): offset = cursor =
+// the running sum.  Each thread scans 4 consecutive counts, the waves by
+// shuffles, the 16 wave totals in LDS (a Hillis-Steele scan with a barrier
+// per step took 9 us for 4,096 counts).
 __global__ void __launch_bounds__(1024)
     kernel_adder_bin_scan(const int *__restrict__ count, int n,
                           int *__restrict__ offset, int *__restrict__ cursor) {
-  __shared__ int part[1024];
-  const int tid = threadIdx.x;
+  __shared__ int wave_sum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int running = 0;
-  for (int base = 0; base < n; base += 1024) {
-    const int v = base + tid < n ? count[base + tid] : 0;
-    part[tid] = v;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-      const int add = tid >= d ? part[tid - d] : 0;
-      __syncthreads();
-      part[tid] += add;
-      __syncthreads();
+  for (int base = 0; base < n; base += 4096) {
+    int v[4], t = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + 4 * tid + j;
+      v[j] = i < n ? count[i] : 0;
+      t += v[j];
     }
-    if (base + tid < n) {
-      offset[base + tid] = running + part[tid] - v;
-      cursor[base + tid] = running + part[tid] - v;
+    int incl = t;  // inclusive scan of the thread totals within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(incl, d);
+      if (lane >= d) incl += o;
     }
-    running += part[1023];
+    if (lane == 63) wave_sum[wave] = incl;
     __syncthreads();
+    int before = running;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) before += w < wave ? wave_sum[w] : 0;
+    int total = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) total += wave_sum[w];
+    int e = before + incl - t;  // exclusive prefix of this thread's first
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + 4 * tid + j;
+      if (i < n) {
+        offset[i] = e;
+        cursor[i] = e;
+      }
+      e += v[j];
+    }
+    running += total;
+    __syncthreads();  // wave_sum is rewritten by the next chunk
   }
 }
 
@@ -233,10 +261,13 @@ __global__ void __launch_bounds__(256)
   __shared__ float2 table[kAddMaxTable];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntx = (G + kAddTile - 1) / kAddTile;
-  const int tx0 = (blockIdx.x % ntx) * kAddTile;
-  const int ty0 = (blockIdx.x / ntx) * kAddTile;
+  // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal neighbours,
+  // whose subgrid reads share cache lines, run on the same XCD's L2
+  const int tl = xcd_subgrid(blockIdx.x, gridDim.x);
+  const int tx0 = (tl % ntx) * kAddTile;
+  const int ty0 = (tl / ntx) * kAddTile;
   const int z = blockIdx.y;
-  const int tile = z * ntx * ntx + blockIdx.x;
+  const int tile = z * ntx * ntx + tl;
   const int npix = S * S;
   const bool tabled = 2 * S - 1 <= kAddMaxTable;
   // shift phasor depends on x + y only
@@ -297,26 +328,20 @@ __global__ void __launch_bounds__(256)
 
   const int n = count[tile];
   if (n <= kAddBinCap) {
-    // the bin, sorted ascending (bitonic over the next power of two)
-    int n2 = 1;
-    while (n2 < n) n2 <<= 1;
+    // the bin sorted ascending by rank (subgrid indices are distinct): each
+    // entry's rank = the entries below it, one barrier (a bitonic sort
+    // took one per stage, 21 for a bin of 64)
     const int off = offset[tile];
-    for (int i = tid; i < n2; i += 256) keys[i] = i < n ? list[off + i] : 0x7fffffff;
+    int *raw = reinterpret_cast<int *>(corner);  // staging, then corners
+    for (int i = tid; i < n; i += 256) raw[i] = list[off + i];
     __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < n2; i += 256) {
-          const int l = i ^ j;
-          if (l > i) {
-            const int a = keys[i], b = keys[l];
-            if (((i & k) == 0) == (a > b)) {
-              keys[i] = b;
-              keys[l] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
+    for (int i = tid; i < n; i += 256) {
+      const int key = raw[i];
+      int rank = 0;
+      for (int j = 0; j < n; ++j) rank += raw[j] < key;
+      keys[rank] = key;
+    }
+    __syncthreads();
     for (int e = tid; e < n; e += 256) {
       const idg::Metadata m = metadata[keys[e]];
       corner[e] = make_int2(m.coordinate.x, m.coordinate.y);
@@ -373,15 +398,44 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The splitter's processing order: subgrids counting-sorted by the grid
+// tile holding their corner (w-layer major, then tile rows), those not
+// wholly inside the grid last.  Consecutive workgroups of one XCD
+// (xcd_subgrid) then read overlapping grid windows, which stay in that XCD's
+// L2, instead of every subgrid pulling its 32 KB window from the Infinity
+// Cache.  The order within a tile is that of the atomics; the output does
+// not depend on it (every subgrid is written by its own workgroup).
+__global__ void __launch_bounds__(256)
+    kernel_splitter_key(const idg::Metadata *__restrict__ metadata,
+                        int nr_subgrids, int G, int S, int nr_w_layers,
+                        int pass, int *__restrict__ count,
+                        int *__restrict__ cursor, int *__restrict__ order) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= nr_subgrids) return;
+  const idg::Metadata m = metadata[s];
+  const int ntx = (G + kAddTile - 1) / kAddTile;
+  const int key = fits(m, G, S, nr_w_layers)
+                      ? (m.coordinate.z * ntx + m.coordinate.y / kAddTile) *
+                                ntx +
+                            m.coordinate.x / kAddTile
+                      : nr_w_layers * ntx * ntx;
+  if (pass == 0)
+    atomicAdd(count + key, 1);
+  else
+    order[atomicAdd(cursor + key, 1)] = s;
+}
+
 // F[s][pol][ys][xs] = conj(shift_phasor(x, y)) * grid[z][pol][cy + y][cx + x]
 // (zero when the subgrid does not lie inside the grid).
 __global__ void __launch_bounds__(256)
     kernel_splitter(const idg::Metadata *__restrict__ metadata,
+                    const int *__restrict__ order,
                     const float2 *__restrict__ grid,
                     float2 *__restrict__ subgrids, int G, int S,
                     int nr_w_layers) {
   __shared__ float2 table[kAddMaxTable];
-  const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int s = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  const int tid = threadIdx.x, nt = blockDim.x;
   const idg::Metadata m = metadata[s];
   const bool inside = fits(m, G, S, nr_w_layers);
   const int npix = S * S;
@@ -424,6 +478,7 @@ __global__ void __launch_bounds__(256)
 template <int S>
 __global__ void __launch_bounds__(256)
     kernel_splitter_pairs(const idg::Metadata *__restrict__ metadata,
+                          const int *__restrict__ order,
                           const float2 *__restrict__ grid,
                           float4 *__restrict__ subgrids, int G,
                           int nr_w_layers) {
@@ -431,7 +486,8 @@ __global__ void __launch_bounds__(256)
   constexpr int PR = S * S / 2 / 256;  // pairs per thread
   constexpr int npix = S * S;
   __shared__ float2 table[2 * S - 1];
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int s = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  const int tid = threadIdx.x;
   const idg::Metadata m = metadata[s];
   const bool inside = fits(m, G, S, nr_w_layers);
   for (int k = tid; k < 2 * S - 1; k += 256)
@@ -684,7 +740,9 @@ hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
   int *count = ws, *offset = ws + ntiles, *cursor = ws + 2 * ntiles;
   int *list = ws + 3 * ntiles;
   const auto *md = static_cast<const idg::Metadata *>(d_metadata);
-  const int nb = (nr_subgrids + 255) / 256;
+  // one thread per (subgrid, tile of its span x span window)
+  const int nb = static_cast<int>(
+      (static_cast<long long>(nr_subgrids) * span * span + 255) / 256);
   err = hipMemsetAsync(count, 0, ntiles * sizeof(int), stream);
   if (err == hipSuccess) {
     hipLaunchKernelGGL(kernel_adder_bin, dim3(nb), dim3(256), 0, stream, md,
@@ -711,21 +769,45 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
                            const void *d_grid, void *d_subgrids,
                            hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
-  if (subgrid_size == 32 || subgrid_size == 64) {
-    hipLaunchKernelGGL(
-        subgrid_size == 32 ? kernel_splitter_pairs<32> : kernel_splitter_pairs<64>,
-        dim3(nr_subgrids), dim3(256), 0, stream,
-        static_cast<const idg::Metadata *>(d_metadata),
-        static_cast<const float2 *>(d_grid), static_cast<float4 *>(d_subgrids),
-        grid_size, nr_w_layers);
-    return hipGetLastError();
+  const int ntx = (grid_size + kAddTile - 1) / kAddTile;
+  const int nkeys = std::max(0, nr_w_layers) * ntx * ntx + 1;
+  // stream-ordered workspace: count | offset | cursor | order
+  int *ws = nullptr;
+  hipError_t err = hipMallocAsync(
+      reinterpret_cast<void **>(&ws),
+      (3 * static_cast<size_t>(nkeys) + nr_subgrids) * sizeof(int), stream);
+  if (err != hipSuccess) return err;
+  int *count = ws, *offset = ws + nkeys, *cursor = ws + 2 * nkeys;
+  int *order = ws + 3 * nkeys;
+  const auto *md = static_cast<const idg::Metadata *>(d_metadata);
+  const int nb = (nr_subgrids + 255) / 256;
+  err = hipMemsetAsync(count, 0, nkeys * sizeof(int), stream);
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL(kernel_splitter_key, dim3(nb), dim3(256), 0, stream,
+                       md, nr_subgrids, grid_size, subgrid_size, nr_w_layers,
+                       0, count, cursor, order);
+    hipLaunchKernelGGL(kernel_adder_bin_scan, dim3(1), dim3(1024), 0, stream,
+                       count, nkeys, offset, cursor);
+    hipLaunchKernelGGL(kernel_splitter_key, dim3(nb), dim3(256), 0, stream,
+                       md, nr_subgrids, grid_size, subgrid_size, nr_w_layers,
+                       1, count, cursor, order);
+    if (subgrid_size == 32 || subgrid_size == 64)
+      hipLaunchKernelGGL(subgrid_size == 32 ? kernel_splitter_pairs<32>
+                                            : kernel_splitter_pairs<64>,
+                         dim3(nr_subgrids), dim3(256), 0, stream, md, order,
+                         static_cast<const float2 *>(d_grid),
+                         static_cast<float4 *>(d_subgrids), grid_size,
+                         nr_w_layers);
+    else
+      hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0,
+                         stream, md, order,
+                         static_cast<const float2 *>(d_grid),
+                         static_cast<float2 *>(d_subgrids), grid_size,
+                         subgrid_size, nr_w_layers);
+    err = hipGetLastError();
   }
-  hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0, stream,
-                     static_cast<const idg::Metadata *>(d_metadata),
-                     static_cast<const float2 *>(d_grid),
-                     static_cast<float2 *>(d_subgrids), grid_size,
-                     subgrid_size, nr_w_layers);
-  return hipGetLastError();
+  const hipError_t ferr = hipFreeAsync(ws, stream);
+  return err != hipSuccess ? err : ferr;
 }
 
 }  // namespace idg_mi355x

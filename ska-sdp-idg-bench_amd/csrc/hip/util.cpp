@@ -73,18 +73,21 @@ void print_dimensions(dim3 g, dim3 b) {
 }
 
 namespace {
-// The timed loop of p_run_kernel over one or more launches per iteration
-// (the two-launch form of the MI355X kernels, util.hpp KernelChoice::parts).
-double time_launches(const idg_mi355x::KernelChoice::Part *parts, int n,
-                     dim3 gridDim, void **args, const std::string &func_name,
-                     double gflops, double gbytes, double mvis) {
+// The timed loop of p_run_kernel: one kernel per iteration, or the
+// two-kernel form of the MI355X kernels (util.hpp KernelChoice::parts).
+double time_launches(const idg_mi355x::KernelChoice &k, dim3 gridDim,
+                     void **args, const std::string &func_name, double gflops,
+                     double gbytes, double mvis) {
   const int warm = static_cast<int>(get_env_var("NR_WARM_UP_RUNS", 2));
   const int iters =
       std::max(1, static_cast<int>(get_env_var("NR_ITERATIONS", 5)));
   auto once = [&] {
-    for (int j = 0; j < n; ++j)
-      hipCheck(idg_mi355x::launch_part(parts[j], static_cast<int>(gridDim.x),
-                                       args, nullptr));
+    if (k.parts[1].func)
+      hipCheck(idg_mi355x::launch_parts(k, static_cast<int>(gridDim.x), args,
+                                        nullptr));
+    else
+      hipCheck(hipLaunchKernel(k.func, gridDim, dim3(k.block), args, 0,
+                               nullptr));
   };
   hipEvent_t start, stop;
   hipCheck(hipEventCreate(&start));
@@ -110,11 +113,10 @@ double time_launches(const idg_mi355x::KernelChoice::Part *parts, int n,
 double p_run_kernel(const void *func, dim3 gridDim, dim3 blockDim,
                     void **args, std::string func_name, double gflops,
                     double gbytes, double mvis) {
-  const idg_mi355x::KernelChoice::Part part{func,
-                                            static_cast<int>(blockDim.x),
-                                            false};
-  return time_launches(&part, 1, gridDim, args, func_name, gflops, gbytes,
-                       mvis);
+  idg_mi355x::KernelChoice k;
+  k.func = func;
+  k.block = static_cast<int>(blockDim.x);
+  return time_launches(k, gridDim, args, func_name, gflops, gbytes, mvis);
 }
 
 void c_run_kernel(const void *func, dim3 gridDim, dim3 blockDim, void **args) {
@@ -274,15 +276,10 @@ hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
                   &d_uvw,         &d_wavenumbers,   &d_visibilities,
                   &d_spheroidal,  &d_aterms,        &d_metadata,
                   &d_subgrids};
-  if (force || k.parts[0].func == nullptr)
+  if (force || k.parts[1].func == nullptr)
     return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args,
                            0, stream);
-  for (const KernelChoice::Part &part : k.parts) {
-    if (part.func == nullptr) continue;
-    const hipError_t err = launch_part(part, p.nr_subgrids, args, stream);
-    if (err != hipSuccess) return err;
-  }
-  return hipSuccess;
+  return launch_parts(k, p.nr_subgrids, args, stream);
 }
 
 namespace {
@@ -303,25 +300,43 @@ int resident_workgroups(const void *func, int block) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
                             dev) != hipSuccess)
     return 0;
+  // IDG_PERSISTENT_PER_CU overrides the occupancy query (A/B)
+  if (const char *v = std::getenv("IDG_PERSISTENT_PER_CU")) per_cu = std::atoi(v);
   const int n = std::max(1, per_cu) * std::max(1, cus);
+  if (std::getenv("IDG_DEBUG_LAUNCH"))
+    std::fprintf(stderr, "idg-mi355x: persistent grid %d (%d per CU x %d CUs)\n",
+                 n, per_cu, cus);
   cache[key] = n;
   return n;
 }
 }  // namespace
 
-hipError_t launch_part(const KernelChoice::Part &part, int nr_subgrids,
-                       void **args13, hipStream_t stream) {
-  if (!part.persistent)
-    return hipLaunchKernel(part.func, dim3(nr_subgrids), dim3(part.block),
-                           args13, 0, stream);
-  const int resident = resident_workgroups(part.func, part.block);
+hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
+                        hipStream_t stream) {
+  if (nr_subgrids <= 0) return hipSuccess;
+  const KernelChoice::Part &mirror = k.parts[0], &general = k.parts[1];
+  const int resident = resident_workgroups(general.func, general.block);
   if (resident <= 0) return hipErrorInvalidConfiguration;
-  int ns = nr_subgrids;
-  void *args14[14];
-  for (int i = 0; i < 13; ++i) args14[i] = args13[i];
-  args14[13] = &ns;
-  return hipLaunchKernel(part.func, dim3(std::min(nr_subgrids, resident)),
-                         dim3(part.block), args14, 0, stream);
+  int *queue = nullptr;
+  hipError_t err = hipMallocAsync(
+      reinterpret_cast<void **>(&queue),
+      (static_cast<size_t>(nr_subgrids) + 2) * sizeof(int), stream);
+  if (err != hipSuccess) return err;
+  err = hipMemsetAsync(queue, 0, 2 * sizeof(int), stream);
+  int ns = nr_subgrids, all = mirror.func ? 0 : 1;
+  void *args[16];
+  for (int i = 0; i < 13; ++i) args[i] = args13[i];
+  args[13] = &queue;
+  if (err == hipSuccess && mirror.func)
+    err = hipLaunchKernel(mirror.func, dim3(nr_subgrids), dim3(mirror.block),
+                          args, 0, stream);
+  args[14] = &ns;
+  args[15] = &all;
+  if (err == hipSuccess)
+    err = hipLaunchKernel(general.func, dim3(std::min(nr_subgrids, resident)),
+                          dim3(general.block), args, 0, stream);
+  const hipError_t ferr = hipFreeAsync(queue, stream);
+  return err != hipSuccess ? err : ferr;
 }
 
 namespace {
@@ -651,10 +666,9 @@ double run_performance(Direction dir, const void *func, std::string name,
   const KernelChoice k = dir == Direction::kGridder ? select_gridder(p)
                                                     : select_degridder(p);
   double seconds;
-  if (func == k.func && k.parts[0].func) {
-    const int n = k.parts[1].func ? 2 : 1;
-    seconds = hip::time_launches(k.parts, n, dim3(nr_subgrids), args, name,
-                                 gflops, gbytes, mvis);
+  if (func == k.func && k.parts[1].func) {
+    seconds = hip::time_launches(k, dim3(nr_subgrids), args, name, gflops,
+                                 gbytes, mvis);
   } else {
     seconds = hip::p_run_kernel(func, dim3(nr_subgrids), dim3(num_threads),
                                 args, name, gflops, gbytes, mvis);

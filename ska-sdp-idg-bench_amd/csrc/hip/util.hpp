@@ -113,24 +113,27 @@ struct KernelChoice {
   const char *name = "";
   int block = 256;
   int grid = 0;  // = nr_subgrids
-  // The launch the device entries make instead, when set: one kernel per
-  // subgrid class, each with the register allocation of its own path
-  // (DESIGN.md §4.1): the mirror-only kernel over grid = nr_subgrids (a
-  // workgroup whose subgrid is not mirror-eligible returns at once), then
-  // the general-only kernel, `persistent`: a resident grid (occupancy x CUs,
-  // at most nr_subgrids) whose workgroups take contiguous subgrid ranges;
-  // it takes nr_subgrids as a 14th argument.
+  // The launch the device entries make instead, when parts[1] is set: one
+  // kernel per subgrid class, each with the register allocation of its own
+  // path.  parts[0] (kMirror; absent for odd S): grid =
+  // nr_subgrids, the 13-argument ABI plus `int *queue`; it takes the
+  // mirror-eligible subgrids and queues the others.  parts[1] (kGeneral): a
+  // resident grid (occupancy x CUs, at most nr_subgrids), the 13 arguments
+  // plus (int *queue, int nr_subgrids, int all); it takes the queued
+  // subgrids, or all of them when there is no mirror kernel.  queue:
+  // nr_subgrids + 2 ints of stream-ordered workspace, [0..1] zeroed.
+  enum Kind { kPlain = 0, kMirror = 1, kGeneral = 2 };
   struct Part {
     const void *func = nullptr;
     int block = 0;
-    bool persistent = false;
+    int kind = kPlain;
   } parts[2];
 };
 
-// Launch one part of a two-launch kernel choice on `stream`; args13 is the
-// 13-argument kernel ABI (the persistent part gets nr_subgrids appended).
-hipError_t launch_part(const KernelChoice::Part &part, int nr_subgrids,
-                       void **args13, hipStream_t stream);
+// The two-kernel launch of `k` (k.parts[1].func set) on `stream`; args13 is
+// the 13-argument kernel ABI.
+hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
+                        hipStream_t stream);
 
 // Defined in the kernel TUs.
 KernelChoice select_gridder(const Problem &p);

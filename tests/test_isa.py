@@ -124,7 +124,7 @@ def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
             continue
         checked.append(k)
         assert total > 0 and drained == 0, (k, total, drained)
-    assert "gridder<32,4,16,1,4,1>" in checked, checked
+    assert "gridder_mirror<32,16,4>" in checked, checked
     assert "gridder_general<32,16,4>" in checked, checked
 
 
