@@ -650,10 +650,11 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
 // The two-kernel form of the device entries (select_degridder; DESIGN.md
 // §4.2), as the gridder's (gridder_mi355x.hip.cpp): the mirror kernel,
 // grid = nr_subgrids, degrids the mirror-eligible subgrids and queues the
-// others (queue[0] = count, queue[2 + i] = subgrid); the general kernel, a
-// resident grid of 8-wave workgroups, takes the queued subgrids one at a
-// time from a shared counter (queue[1]; all subgrids with `all` set, odd S)
-// and degrids each with chunks of KP = 1,024 single pixels (one thread per
+// others (device.hpp: queue_push); the general kernel, a resident grid of
+// 8-wave workgroups, takes the queued subgrids one at a time from the
+// queue's take counter (all subgrids, with no mirror launch, when `all` is
+// set: odd S or w_step_in_lambda != 0) and degrids each with chunks of
+// KP = 1,024 single pixels (one thread per
 // K-block of the 512), so an S = 32 subgrid is one chunk and its
 // visibilities are written once (the combined kernel's 512-pixel chunks
 // read them back and wrote them again).
@@ -688,7 +689,7 @@ __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
   const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
   __syncthreads();
   if (!eligible) {
-    if (tid == 0) queue[2 + atomicAdd(queue, 1)] = s;
+    if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
   degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
@@ -715,17 +716,19 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
   const int tid = threadIdx.x;
-  const int count = all ? nr_subgrids : queue[0];
+  const QueueView qv = queue_view(queue, nr_subgrids);
+  const int count = all ? nr_subgrids : qv.count();
   // the next queue position, taken by thread 0 and passed on through lds[0]
   // (between subgrids, where degrid_mfma uses no LDS)
-  if (tid == 0) lds[0] = static_cast<unsigned>(atomicAdd(queue + 1, 1));
+  if (tid == 0)
+    lds[0] = static_cast<unsigned>(atomicAdd(queue + kQueueNext, 1));
   __syncthreads();
   int i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
   __syncthreads();
   while (i < count) {
     int next = 0;
-    if (tid == 0) next = atomicAdd(queue + 1, 1);  // lands during the subgrid
-    const int s = all ? i : queue[2 + i];
+    if (tid == 0) next = atomicAdd(queue + kQueueNext, 1);  // lands later
+    const int s = all ? i : qv.at(i);
     const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
                                          image_size, w_step_in_lambda);
     degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
@@ -738,6 +741,38 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
     __syncthreads();
   }
+}
+
+// The general path alone, one 8-wave workgroup per subgrid with KP = 1,024
+// (grid = nr_subgrids, the 13-argument ABI): the device entries' launch
+// when no subgrid can be mirror-eligible (odd S, or w_step_in_lambda != 0:
+// every w_offset is then non-zero).  The general path is the generic
+// computation, valid for any subgrid.  On a w-term batch this runs 2-3 %
+// faster than the queue-fed general kernel above, whose workgroups loop
+// over subgrids.
+template <int S_CT, int CT>
+__global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
+    kernel_degridder_general_direct_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        const float2 *__restrict__ subgrids) {
+  constexpr int NW = 8, KP = 1024;
+  __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
+  const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
+                                       w_step_in_lambda);
+  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+      g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+      visibilities, spheroidal, aterms,
+      subgrids + static_cast<size_t>(s) * 4 * npix, lds);
 }
 
 #define IDG_DEGRIDDER(S_, CG_, MODE_, NW_) \
@@ -784,7 +819,7 @@ KernelChoice select_degridder(const Problem &p) {
     // the MFMA kernel has no CG
     k.func = nw8 ? IDG_PICK(4, 1, 8) : IDG_PICK(4, 1, 4);
     k.block = nw8 ? 512 : 256;
-    if (IDG_DEGRID_SPLIT) {
+    if (IDG_DEGRID_SPLIT && !combined_form()) {
       // mirror-eligible subgrids (even S only), then the others on 8-wave
       // workgroups with 1,024-pixel chunks
 #define IDG_PICK_MIRROR(NW_)                                               \
@@ -797,6 +832,14 @@ KernelChoice select_degridder(const Problem &p) {
                         : (s64 ? IDG_DEGRIDDER_GENERAL(64)
                                : IDG_DEGRIDDER_GENERAL(0)),
                     512, KernelChoice::kGeneral};
+      k.all_general = {
+          reinterpret_cast<const void *>(
+              s32 ? &kernel_degridder_general_direct_mi355x<32, IDG_DEGRID_CT>
+                  : (s64 ? &kernel_degridder_general_direct_mi355x<
+                               64, IDG_DEGRID_CT>
+                         : &kernel_degridder_general_direct_mi355x<
+                               0, IDG_DEGRID_CT>)),
+          512, KernelChoice::kPlain};
 #undef IDG_PICK_MIRROR
     }
   } else {

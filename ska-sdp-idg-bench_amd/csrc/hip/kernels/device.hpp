@@ -129,6 +129,54 @@ __device__ __forceinline__ int xcd_subgrid(int orig, int nwg) {
 #endif
 }
 
+// The general-subgrid queue of the two-kernel launch (util.hpp
+// KernelChoice::parts): the mirror kernel pushes the subgrids it leaves,
+// the general kernel takes them from a shared counter.  8 shards, one per
+// XCD (the pushing workgroup's blockIdx % 8, so at most ceil(NS / 8) pushes
+// each), each a count on a 128-byte line of its own (a single count took
+// 0.28 ms of serialized atomics for 24,500 pushes) and a list; then one take
+// counter.  Layout in ints: counts at 32 x, take counter at kQueueNext,
+// shard x's list at kQueueHead + x * queue_cap(ns); ints [0, kQueueNext]
+// are zeroed before the launches.
+constexpr int kQueueShards = 8, kQueueNext = 256, kQueueHead = 288;
+
+__host__ __device__ inline int queue_cap(int ns) {
+  return (ns + kQueueShards - 1) / kQueueShards;
+}
+__host__ __device__ inline size_t queue_ints(int ns) {
+  return kQueueHead + static_cast<size_t>(kQueueShards) * queue_cap(ns);
+}
+
+// One thread of the pushing workgroup.
+__device__ __forceinline__ void queue_push(int *queue, int ns, int s) {
+  const int x = blockIdx.x % kQueueShards;
+  queue[kQueueHead + x * queue_cap(ns) + atomicAdd(queue + 32 * x, 1)] = s;
+}
+
+// The queue's entries in shard order: count() of them, at(i) the i-th.
+struct QueueView {
+  const int *q;
+  int cap, pre[kQueueShards + 1];
+  __device__ int count() const { return pre[kQueueShards]; }
+  __device__ int at(int i) const {
+    int x = 0;
+#pragma unroll
+    for (int k = 1; k < kQueueShards; ++k) x += i >= pre[k] ? 1 : 0;
+    return q[kQueueHead + x * cap + (i - pre[x])];
+  }
+};
+
+__device__ __forceinline__ QueueView queue_view(const int *queue, int ns) {
+  QueueView v;
+  v.q = queue;
+  v.cap = queue_cap(ns);
+  v.pre[0] = 0;
+#pragma unroll
+  for (int x = 0; x < kQueueShards; ++x)
+    v.pre[x + 1] = v.pre[x] + __builtin_amdgcn_readfirstlane(queue[32 * x]);
+  return v;
+}
+
 // Per-subgrid constants, evaluated exactly as the reference does
 // (gridder_reference.cpp:15-39): offsets in double, rounded to float.
 struct SubgridSetup {

@@ -833,18 +833,20 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 // kernel_gridder_mirror_mi355x: grid = nr_subgrids, one workgroup per
 //   subgrid as kernel_gridder_mi355x; a mirror-eligible subgrid (even S,
 //   w_offset = 0, w = 0 on every timestep) is gridded on the mirror GEMMs,
-//   any other is appended to the general queue (queue[0] = count,
-//   queue[2 + i] = subgrid) and left.
+//   any other is pushed onto the general queue (device.hpp: queue_push) and
+//   left.
 // kernel_gridder_general_mi355x: a resident grid (occupancy x CUs) that
-//   takes the queued subgrids one at a time from a shared counter
-//   (queue[1]), the next index requested while the current subgrid runs,
-//   and grids each on the fused single-pixel GEMMs; with `all` set (odd S:
-//   no subgrid is mirror-eligible, no mirror launch) it takes subgrids
-//   0 .. nr_subgrids-1 instead.  Dynamic, not a fixed range per workgroup:
-//   with fixed ranges the slowest CU set the time (w-term batch +7-9 %).
-//   On a batch without w-terms the queue is empty and every workgroup
-//   returns at once.
-// queue: nr_subgrids + 2 ints, queue[0..1] zeroed before the launches.
+//   takes the queued subgrids one at a time from the queue's take counter,
+//   the next index requested while the current subgrid runs, and grids each
+//   on the fused single-pixel GEMMs.  With `all` set it takes subgrids
+//   0 .. nr_subgrids-1 and there is no mirror launch: the launch layer sets
+//   it when no subgrid can be mirror-eligible (odd S, or w_step_in_lambda
+//   != 0, which makes every w_offset non-zero).  Dynamic, not a fixed range
+//   per workgroup: with fixed ranges the slowest CU set the time (w-term
+//   batch +7-9 %).  On a batch without w-terms the queue is empty and every
+//   workgroup returns at once.
+// queue: device.hpp queue_ints(nr_subgrids) ints of stream-ordered
+// workspace, its counters zeroed before the launches.
 template <int S_CT, int CB, int PT>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     kernel_gridder_mirror_mi355x(
@@ -871,7 +873,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
   const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
                       g.w_offset == 0.0f;
   if (!mirror) {
-    if (tid == 0) queue[2 + atomicAdd(queue, 1)] = s;
+    if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
   grid_mfma<S_CT, PT, CB, NW, true>(
@@ -898,17 +900,19 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
   const int tid = threadIdx.x;
-  const int count = all ? nr_subgrids : queue[0];
+  const QueueView qv = queue_view(queue, nr_subgrids);
+  const int count = all ? nr_subgrids : qv.count();
   // the next queue position, taken by thread 0 and passed on through lds[0]
   // (between subgrids, where grid_mfma uses no LDS)
-  if (tid == 0) lds[0] = static_cast<unsigned>(atomicAdd(queue + 1, 1));
+  if (tid == 0)
+    lds[0] = static_cast<unsigned>(atomicAdd(queue + kQueueNext, 1));
   __syncthreads();
   int i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
   __syncthreads();
   while (i < count) {
     int next = 0;
-    if (tid == 0) next = atomicAdd(queue + 1, 1);  // lands during the subgrid
-    const int s = all ? i : queue[2 + i];
+    if (tid == 0) next = atomicAdd(queue + kQueueNext, 1);  // lands later
+    const int s = all ? i : qv.at(i);
     const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
                                          image_size, w_step_in_lambda);
     grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
@@ -971,9 +975,12 @@ KernelChoice select_gridder(const Problem &p) {
       part[1] = IDG_GRIDDER_GENERAL(0);
       break;
   }
-  if (mfma && IDG_GRID_SPLIT) {
+  if (mfma && IDG_GRID_SPLIT && !combined_form()) {
     if (part[0]) k.parts[0] = {part[0], k.block, KernelChoice::kMirror};
     k.parts[1] = {part[1], k.block, KernelChoice::kGeneral};
+    // no subgrid mirror-eligible: the combined kernel, one workgroup per
+    // subgrid (2.7 % faster on a w-term batch than the queue-fed kernel)
+    k.all_general = {k.func, k.block, KernelChoice::kPlain};
   }
   return k;
 }

@@ -14,6 +14,7 @@
 #include <utility>
 
 #include "lib-hip.hpp"
+#include "hip/kernels/device.hpp"
 
 namespace hip {
 
@@ -83,8 +84,9 @@ double time_launches(const idg_mi355x::KernelChoice &k, dim3 gridDim,
       std::max(1, static_cast<int>(get_env_var("NR_ITERATIONS", 5)));
   auto once = [&] {
     if (k.parts[1].func)
-      hipCheck(idg_mi355x::launch_parts(k, static_cast<int>(gridDim.x), args,
-                                        nullptr));
+      hipCheck(idg_mi355x::launch_parts(
+          k, static_cast<int>(gridDim.x), args,
+          *static_cast<float *>(args[3]) != 0.0f, nullptr));
     else
       hipCheck(hipLaunchKernel(k.func, gridDim, dim3(k.block), args, 0,
                                nullptr));
@@ -221,6 +223,11 @@ void print_benchmark() {
 
 namespace idg_mi355x {
 
+bool combined_form() {
+  const char *v = std::getenv("IDG_KERNEL_FORM");
+  return v != nullptr && std::string(v) == "combined";
+}
+
 std::string validate(const Problem &p, const Extents &e,
                      const idg::Metadata *md) {
   std::ostringstream err;
@@ -279,7 +286,8 @@ hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
   if (force || k.parts[1].func == nullptr)
     return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args,
                            0, stream);
-  return launch_parts(k, p.nr_subgrids, args, stream);
+  return launch_parts(k, p.nr_subgrids, args, p.w_step_in_lambda != 0.0f,
+                      stream);
 }
 
 namespace {
@@ -312,22 +320,26 @@ int resident_workgroups(const void *func, int block) {
 }  // namespace
 
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
-                        hipStream_t stream) {
+                        bool all_general, hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
   const KernelChoice::Part &mirror = k.parts[0], &general = k.parts[1];
+  if ((all_general || mirror.func == nullptr) && k.all_general.func)
+    return hipLaunchKernel(k.all_general.func, dim3(nr_subgrids),
+                           dim3(k.all_general.block), args13, 0, stream);
   const int resident = resident_workgroups(general.func, general.block);
   if (resident <= 0) return hipErrorInvalidConfiguration;
   int *queue = nullptr;
-  hipError_t err = hipMallocAsync(
-      reinterpret_cast<void **>(&queue),
-      (static_cast<size_t>(nr_subgrids) + 2) * sizeof(int), stream);
+  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&queue),
+                                  queue_ints(nr_subgrids) * sizeof(int),
+                                  stream);
   if (err != hipSuccess) return err;
-  err = hipMemsetAsync(queue, 0, 2 * sizeof(int), stream);
-  int ns = nr_subgrids, all = mirror.func ? 0 : 1;
+  err = hipMemsetAsync(queue, 0, (kQueueNext + 1) * sizeof(int), stream);
+  const bool run_mirror = mirror.func != nullptr && !all_general;
+  int ns = nr_subgrids, all = run_mirror ? 0 : 1;
   void *args[16];
   for (int i = 0; i < 13; ++i) args[i] = args13[i];
   args[13] = &queue;
-  if (err == hipSuccess && mirror.func)
+  if (err == hipSuccess && run_mirror)
     err = hipLaunchKernel(mirror.func, dim3(nr_subgrids), dim3(mirror.block),
                           args, 0, stream);
   args[14] = &ns;

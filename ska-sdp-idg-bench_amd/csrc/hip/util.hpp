@@ -120,20 +120,28 @@ struct KernelChoice {
   // mirror-eligible subgrids and queues the others.  parts[1] (kGeneral): a
   // resident grid (occupancy x CUs, at most nr_subgrids), the 13 arguments
   // plus (int *queue, int nr_subgrids, int all); it takes the queued
-  // subgrids, or all of them when there is no mirror kernel.  queue:
-  // nr_subgrids + 2 ints of stream-ordered workspace, [0..1] zeroed.
+  // subgrids (all of them with `all` set and no mirror launch).  queue:
+  // device.hpp queue_ints(nr_subgrids) ints of stream-ordered workspace.
+  // When no subgrid can be mirror-eligible (odd S, or w_step_in_lambda !=
+  // 0), all_general is launched instead, once: grid = nr_subgrids, the
+  // 13-argument ABI, one workgroup per subgrid on the general path.
   enum Kind { kPlain = 0, kMirror = 1, kGeneral = 2 };
   struct Part {
     const void *func = nullptr;
     int block = 0;
     int kind = kPlain;
-  } parts[2];
+  } parts[2], all_general;
 };
 
 // The two-kernel launch of `k` (k.parts[1].func set) on `stream`; args13 is
-// the 13-argument kernel ABI.
+// the 13-argument kernel ABI.  all_general: no subgrid can be
+// mirror-eligible (w_step_in_lambda != 0), so the mirror launch is skipped.
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
-                        hipStream_t stream);
+                        bool all_general, hipStream_t stream);
+
+// IDG_KERNEL_FORM=combined: the device entries launch the one combined
+// kernel instead of the two-kernel form (A/B and tests; read per call).
+bool combined_form();
 
 // Defined in the kernel TUs.
 KernelChoice select_gridder(const Problem &p);

@@ -370,6 +370,22 @@ def full_w(idg):
     return p, a, _to_device(a)
 
 
+@pytest.fixture(scope="module")
+def full_mixed(idg):
+    """configs[1] sizes with w != 0 on every third subgrid and W_STEP = 0:
+    the two-kernel launch runs both kernels, the mirror one queueing 8,167
+    general subgrids over the queue's 8 shards (device.hpp queue_push)."""
+    st, ts, T, C, G, S = 50, 20, 128, 16, 1024, 32
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    rng = np.random.default_rng(11)
+    a["uvw"][1::3, :, 2] = rng.uniform(-200.0, 200.0,
+                                       a["uvw"][1::3, :, 2].shape)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    return p, a, _to_device(a)
+
+
 def _dgrid(idg, p, dev, vis, md=None):
     import torch
     out = torch.empty((p["nr_subgrids"], 4, p["subgrid_size"],
@@ -584,17 +600,19 @@ def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib):
 
 
 @pytest.mark.parametrize("op", ["gridder", "degridder"])
-@pytest.mark.parametrize("data", ["w0", "wterm"])
+@pytest.mark.parametrize("data", ["w0", "wterm", "mixed"])
 def test_full_size_mfma_path_matches_valu_path_every_subgrid(
-        idg, full, full_w, op, data, monkeypatch):
+        idg, full, full_w, full_mixed, op, data, monkeypatch):
     """The f16-split MFMA kernels against the all-f32 VALU kernels on EVERY
     subgrid of the full config, twice (run-to-run bitwise identical).  This
     is the check that caught a schedule-dependent accumulator corruption in
     ~5 % of subgrids which the sampled oracle comparison only hit by luck.
     'w0': the benchmark data (mirror GEMMs); 'wterm': w != 0 everywhere
-    (single-pixel GEMMs with the w-term)."""
+    (single-pixel GEMMs with the w-term; W_STEP != 0, so the general kernel
+    alone); 'mixed': every third subgrid w != 0 with W_STEP = 0 (both
+    kernels of the two-kernel launch, through the general queue)."""
     import torch
-    p, a, dev = full if data == "w0" else full_w
+    p, a, dev = {"w0": full, "wterm": full_w, "mixed": full_mixed}[data]
     env = "IDG_GRIDDER_IMPL" if op == "gridder" else "IDG_DEGRIDDER_IMPL"
     run = ((lambda: _dgrid(idg, p, dev, dev["visibilities"]))
            if op == "gridder" else
@@ -808,3 +826,32 @@ def test_perf_mode_reports_the_kernel_rate(event_rates, harness, direction,
     assert f"{direction}_mi355x" in out
     assert abs(mvis / event_rates[direction] - 1.0) <= 0.05, (
         mvis, event_rates[direction])
+
+
+@pytest.mark.parametrize("op", ["gridder", "degridder"])
+@pytest.mark.parametrize("data", ["w0", "mixed", "wterm"])
+def test_two_kernel_launch_matches_combined_kernel(idg, full, full_w,
+                                                   full_mixed, op, data,
+                                                   monkeypatch):
+    """The device entries' two-kernel launch (mirror kernel + general kernel
+    fed by the queue) against the one combined kernel
+    (IDG_KERNEL_FORM=combined) on every subgrid of the full config.  Mirror
+    subgrids and the gridder's general ones run the same code: bitwise.  The
+    degridder's general kernel sums 1,024-pixel chunks where the combined one
+    sums two of 512: within the parity bar."""
+    import torch
+    p, a, dev = {"w0": full, "wterm": full_w, "mixed": full_mixed}[data]
+    run = ((lambda: _dgrid(idg, p, dev, dev["visibilities"]))
+           if op == "gridder" else
+           (lambda: _ddegrid(idg, p, dev, dev["subgrids"])))
+    two = run()
+    monkeypatch.setenv("IDG_KERNEL_FORM", "combined")
+    one = run()
+    torch.cuda.synchronize()
+    if op == "gridder" or data == "w0":
+        assert torch.equal(two, one)
+    else:
+        ns = one.shape[0]
+        diff = (two.double() - one.double()).reshape(ns, -1).abs().amax(1)
+        mag = one.double().reshape(ns, -1).abs().amax(1)
+        assert float((diff / mag).max()) <= TOLERANCE
