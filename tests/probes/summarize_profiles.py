@@ -32,14 +32,39 @@ CYC_TRANS, CYC_MFMA_F16, CYC_VALU = 8.35, 4.7, 4.46
 N_SIMD, N_XCD = 1024, 8
 
 
+KERNELS = (  # name tag -> (direction, variant); S is the first template arg
+    ("kernel_gridder_mirror_mi355x<", "gridder", "mirror"),
+    ("kernel_gridder_general_mi355x<", "gridder", "general_queue"),
+    ("kernel_gridder_mi355x<", "gridder", "combined"),
+    ("kernel_degridder_mirror_mi355x<", "degridder", "mirror"),
+    ("kernel_degridder_general_direct_mi355x<", "degridder", "general_direct"),
+    ("kernel_degridder_general_mi355x<", "degridder", "general_queue"),
+    ("kernel_degridder_mi355x<", "degridder", "combined"),
+)
+PIPELINE = ("kernel_subgrid_fft_reg", "kernel_subgrid_fft2", "kernel_subgrid_dft",
+            "kernel_adder_bin_scan", "kernel_adder_bin", "kernel_adder",
+            "kernel_splitter_key", "kernel_splitter_pairs", "kernel_splitter")
+
+
 def short_name(kernel_name):
-    """'void idg_mi355x::kernel_gridder_mi355x<32, 4, 16, 1, 4>(...)' ->
-    ('gridder', 32, MODE); None for other kernels."""
-    for d, mode_arg in (("gridder", 3), ("degridder", 2)):
-        tag = f"kernel_{d}_mi355x<"
+    """'void idg_mi355x::kernel_gridder_mirror_mi355x<32, 16, 4>(...)' ->
+    ('gridder', 32, 'mirror'); the combined kernel's VALU instantiation
+    (MODE 0) and other kernels -> None."""
+    for tag, d, variant in KERNELS:
         if tag in kernel_name:
             args = kernel_name.split(tag, 1)[1].split(">", 1)[0].split(",")
-            return d, int(args[0]), int(args[mode_arg])
+            if variant == "combined":
+                mode = int(args[3] if d == "gridder" else args[2])
+                if mode != 1:
+                    return None
+            return d, int(args[0]), variant
+    return None
+
+
+def pipeline_name(kernel_name):
+    for tag in PIPELINE:
+        if "::" + tag + "<" in kernel_name or "::" + tag + "(" in kernel_name:
+            return tag[len("kernel_"):]
     return None
 
 
@@ -66,30 +91,43 @@ def read_rows(path):
 
 
 def kernel_stats(rows):
-    acc = defaultdict(list)
+    """{(bench kernel, variant): duration stats} and the pipeline kernels'
+    {name: stats}."""
+    acc, pipe = defaultdict(list), defaultdict(list)
     for r in rows:
+        dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         k = short_name(r["Kernel_Name"])
-        if k and k[2] == 1:
-            acc[bench_name(k[0], k[1])].append(
-                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    return {n: {"launches": len(v), "mean_ns": sum(v) / len(v),
-                "min_ns": min(v), "max_ns": max(v)} for n, v in acc.items()}
+        if k:
+            acc[(bench_name(k[0], k[1]), k[2])].append(dt)
+        else:
+            pn = pipeline_name(r["Kernel_Name"])
+            if pn:
+                pipe[pn].append(dt)
+
+    def st(v):
+        return {"launches": len(v), "mean_ns": sum(v) / len(v),
+                "min_ns": min(v), "max_ns": max(v)}
+    return ({k: st(v) for k, v in acc.items()},
+            {k: st(v) for k, v in pipe.items()})
 
 
 def counters(rows):
-    """{kernel: {counter: mean over launches}} (values summed per dispatch
-    over the rows rocprofv3 writes per dimension)."""
+    """{(bench kernel, variant) or pipeline name: {counter: mean over
+    launches}} (values summed per dispatch over the rows rocprofv3 writes
+    per dimension)."""
     per = defaultdict(lambda: defaultdict(float))
     for r in rows:
         k = short_name(r["Kernel_Name"])
-        if not (k and k[2] == 1):
+        key = (bench_name(k[0], k[1]), k[2]) if k else \
+            pipeline_name(r["Kernel_Name"])
+        if key is None:
             continue
-        per[(bench_name(k[0], k[1]), r["Dispatch_Id"])][r["Counter_Name"]] += \
+        per[(key, r["Dispatch_Id"])][r["Counter_Name"]] += \
             float(r["Counter_Value"])
     out = defaultdict(lambda: defaultdict(list))
-    for (name, _), cs in per.items():
+    for (key, _), cs in per.items():
         for c, v in cs.items():
-            out[name][c].append(v)
+            out[key][c].append(v)
     return {n: {c: sum(v) / len(v) for c, v in cs.items()}
             for n, cs in out.items()}
 
@@ -109,7 +147,7 @@ def main():
                                            "*.db"), recursive=True)[0],
                     "kernel")
     shutil.copy(ktrace, os.path.join(args.out, "kernel_trace.csv"))
-    stats = kernel_stats(read_rows(ktrace))
+    vstats, pstats = kernel_stats(read_rows(ktrace))
 
     traffic = {}
     for cname, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
@@ -121,11 +159,32 @@ def main():
         for n, cs in counters(read_rows(path)).items():
             traffic.setdefault(n, {})[cname] = cs[cname]
 
-    sq = defaultdict(dict)
+    sq_v = defaultdict(dict)
     for db in sorted(glob.glob(os.path.join(args.pmc, "p*", "**", "*.db"),
                                recursive=True)):
         for n, cs in counters(read_rows(to_csv(db, "counter"))).items():
-            sq[n].update(cs)
+            sq_v[n].update(cs)
+
+    # One step launches every variant of a direction at most once: the
+    # direction's per-launch figures are the sums over its variants.
+    stats, sq, vtraffic = {}, defaultdict(lambda: defaultdict(float)), \
+        defaultdict(lambda: defaultdict(float))
+    for (n, variant), st in vstats.items():
+        s0 = stats.setdefault(n, {"launches": 0, "mean_ns": 0.0,
+                                  "min_ns": 0.0, "max_ns": 0.0,
+                                  "variants": {}})
+        s0["launches"] = max(s0["launches"], st["launches"])
+        for key in ("mean_ns", "min_ns", "max_ns"):
+            s0[key] += st[key]
+        s0["variants"][variant] = round(st["mean_ns"] / 1e6, 4)
+    for key, cs in sq_v.items():
+        if isinstance(key, tuple):
+            for c, v in cs.items():
+                sq[key[0]][c] += v
+    for key, cs in traffic.items():
+        if isinstance(key, tuple):
+            for c, v in cs.items():
+                vtraffic[key[0]][c] += v
 
     with open(args.traffic) as f:
         tj = json.load(f)
@@ -135,7 +194,7 @@ def main():
              f"{'max ms':>8s} {'HBM GB':>8s} {'VALU issue':>10s}"]
     for n in sorted(stats):
         st = stats[n]
-        t = traffic.get(n, {})
+        t = vtraffic.get(n, {})
         hbm = None
         if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
             hbm = int((2 * t["FETCH_SIZE"] + t["WRITE_SIZE"]) * 1024)
@@ -180,6 +239,25 @@ def main():
             f"{st['min_ns'] / 1e6:8.4f} {st['max_ns'] / 1e6:8.4f} "
             f"{(hbm or 0) / 1e9:8.3f} "
             f"{issue['utilization'] if issue else float('nan'):10.3f}")
+        lines.append("    variants (mean ms): " + ", ".join(
+            f"{v} {ms}" for v, ms in sorted(st["variants"].items())))
+    # the pipeline steps either side of the path
+    lines.append("")
+    lines.append(f"{'pipeline kernel':28s} {'launches':>8s} {'mean ms':>9s} "
+                 f"{'min ms':>8s} {'HBM GB':>8s} {'GB/s':>8s}")
+    pipe = {}
+    for n in sorted(pstats):
+        st = pstats[n]
+        t = traffic.get(n, {})
+        hbm = None
+        if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
+            hbm = int((2 * t["FETCH_SIZE"] + t["WRITE_SIZE"]) * 1024)
+        pipe[n] = {"mean_ms": round(st["mean_ns"] / 1e6, 4),
+                   "hbm_bytes_per_launch": hbm}
+        lines.append(f"{n:28s} {st['launches']:8d} {st['mean_ns'] / 1e6:9.4f} "
+                     f"{st['min_ns'] / 1e6:8.4f} {(hbm or 0) / 1e9:8.3f} "
+                     f"{(hbm or 0) / st['mean_ns']:8.1f}")
+    summary["pipeline"] = pipe
     with open(os.path.join(args.out, "pmc_sq_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     with open(os.path.join(args.out, "kernel_stats_summary.txt"), "w") as f:
