@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "../util.hpp"
 #include "common/types.hpp"
@@ -142,75 +144,213 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// grid[z][pol][cy + y][cx + x] += shift_phasor(x, y) * F[s][pol][ys][xs],
-// ys = (y + S/2) % S, xs = (x + S/2) % S.
-//
-// A gather, not a scatter: one workgroup owns one 16 x 16 tile of one
-// w-layer, adds the pixels of the subgrids overlapping it into registers in
-// ascending subgrid order and read-modify-writes the tile once.  Every
-// subgrid pixel is read exactly once over the whole launch, there are no
-// atomics on the grid, and the summation order -- hence every bit of the
-// grid -- is deterministic.  The overlapping subgrids come from per-tile
-// bins (count -> scan -> fill, then sorted in LDS); a bin larger than the
-// LDS list falls back to an ordered scan of all the metadata, which yields
-// the same order.
-#ifndef IDG_ADD_TILE
-#define IDG_ADD_TILE 16
+// The home sort: subgrids counting-sorted by their home tile, the grid tile
+// (TW x TH, w-layer major, then tile rows) holding their corner, with the
+// subgrids not wholly inside the grid last.  offset[key] is the first
+// position of key's subgrids in order[], offset[nkeys] = nr_subgrids.  Both
+// the adder and the splitter read it:
+//  * the adder's tile finds the subgrids overlapping it in the home tiles up
+//    to ceil((S - 1) / TW) tiles left and ceil((S - 1) / TH) tiles up of
+//    itself: one contiguous range of order[] per tile row;
+//  * the splitter processes subgrids in this order, so consecutive
+//    workgroups of one XCD (xcd_subgrid) read overlapping grid windows,
+//    which stay in that XCD's L2, instead of every subgrid pulling its
+//    32 KB window from the Infinity Cache.
+// The order within a home tile is that of the atomics; neither output
+// depends on it (the adder sorts its list by subgrid index, the splitter
+// writes every subgrid from its own workgroup).
+#ifndef IDG_ADD_TW
+#define IDG_ADD_TW 16
+#endif
+#ifndef IDG_ADD_TH
+#define IDG_ADD_TH 16
 #endif
 #ifndef IDG_ADD_U
 #define IDG_ADD_U 4
 #endif
-constexpr int kAddTile = IDG_ADD_TILE;  // grid tile edge (pixels)
-constexpr int kAddPix = kAddTile * kAddTile / 256;  // tile pixels per thread
-constexpr int kAddMaxTable = 256; // shift phasors kept in LDS for S <= 128
-constexpr int kAddBinCap = 2048;  // bin entries sorted in LDS
-static_assert(kAddTile * kAddTile == 256 * kAddPix, "tile = block x pixels");
+constexpr int kTW = IDG_ADD_TW;  // grid tile width (pixels)
+constexpr int kTH = IDG_ADD_TH;  // grid tile height
+constexpr int kAddPix = kTW * kTH / 256;  // tile pixels per thread
+constexpr int kAddMaxTable = 256;  // shift phasors kept in LDS for S <= 128
+constexpr int kAddListCap = 1536;  // candidate entries sorted in LDS
+constexpr int kAddMaxRows = 64;    // home-tile rows a tile gathers from
+constexpr int kNoKey = 0x7fffffff;  // a candidate outside the tile
+constexpr int kSortLdsKeys = 19 * 1024;  // LDS: 2 x 76 KB (place kernel)
+constexpr int kSortMaxChunks = 16;       // workgroups of the LDS sort
+static_assert(kTW * kTH == 256 * kAddPix && (kTW & (kTW - 1)) == 0,
+              "tile = block x pixels, power-of-two width");
 
-struct TileSpan {
-  int tx0, tx1, ty0, ty1;  // inclusive tile ranges a subgrid overlaps
+struct TileGrid {
+  int ntx, nty;
+  __host__ __device__ TileGrid(int G)
+      : ntx(G > 0 ? (G + kTW - 1) / kTW : 0),
+        nty(G > 0 ? (G + kTH - 1) / kTH : 0) {}
+  __host__ __device__ int nkeys(int nr_w_layers) const {
+    return nr_w_layers * nty * ntx + 1;
+  }
 };
 
-__device__ __forceinline__ TileSpan tile_span(const idg::Metadata &m, int S) {
-  return {m.coordinate.x / kAddTile, (m.coordinate.x + S - 1) / kAddTile,
-          m.coordinate.y / kAddTile, (m.coordinate.y + S - 1) / kAddTile};
+__device__ __forceinline__ int home_key(const idg::Metadata &m, int G, int S,
+                                        int nr_w_layers, const TileGrid &tg) {
+  return fits(m, G, S, nr_w_layers)
+             ? (m.coordinate.z * tg.nty + m.coordinate.y / kTH) * tg.ntx +
+                   m.coordinate.x / kTW
+             : nr_w_layers * tg.nty * tg.ntx;
 }
 
-// Bins: count (pass 0) or fill (pass 1) the tiles each subgrid overlaps,
-// one thread per (subgrid, tile of its span x span window) pair, so each
-// thread makes one atomic (a thread per subgrid made up to 9 in a row at
-// S = 32 and took 17 us per pass at configs[1]).
-__global__ void __launch_bounds__(256)
-    kernel_adder_bin(const idg::Metadata *__restrict__ metadata,
-                     int nr_subgrids, int G, int S, int nr_w_layers, int pass,
-                     int *__restrict__ count, int *__restrict__ cursor,
-                     int *__restrict__ list) {
-  const int span = (S + kAddTile - 2) / kAddTile + 1;  // tiles per axis, max
-  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-  const int s = static_cast<int>(i / (span * span));
-  if (s >= nr_subgrids) return;
-  const int k = static_cast<int>(i - static_cast<long long>(s) * span * span);
-  const idg::Metadata m = metadata[s];
-  if (!fits(m, G, S, nr_w_layers)) return;
-  const TileSpan t = tile_span(m, S);
-  const int ty = t.ty0 + k / span, tx = t.tx0 + k % span;
-  if (ty > t.ty1 || tx > t.tx1) return;
-  const int ntx = (G + kAddTile - 1) / kAddTile;
-  const int tile = (m.coordinate.z * ntx + ty) * ntx + tx;
-  if (pass == 0)
-    atomicAdd(count + tile, 1);
-  else
-    list[atomicAdd(cursor + tile, 1)] = s;
+// Exclusive scan of the n values v[0, n) held by one workgroup of 1,024:
+// each thread takes `per` consecutive values, the waves scan their thread
+// totals by shuffles, the 16 wave totals go through LDS.  Returns this
+// thread's exclusive prefix; the caller walks its `per` values from it.
+__device__ __forceinline__ int block_scan_1024(int t, int *wave_sum) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wave_sum[wave] = incl;
+  __syncthreads();
+  int before = incl - t;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) before += w < wave ? wave_sum[w] : 0;
+  return before;
 }
 
-// Exclusive scan of n counts (one workgroup of 1,024): offset = cursor =
-// the running sum.  Each thread scans 4 consecutive counts, the waves by
-// shuffles, the 16 wave totals in LDS (a Hillis-Steele scan with a barrier
-// per step took 9 us for 4,096 counts).
+// The home sort in two launches of nwg workgroups of 1,024, each workgroup
+// owning a contiguous chunk of subgrids, with its counters in LDS (no
+// device-scope atomics, which cross the XCDs: a counting pass of 24,500 of
+// them took 19 us; one workgroup sorting everything took 47 us):
+//  count: key and rank within the chunk's home tile -> slot[s], the chunk's
+//         histogram -> hist[key][w];
+//  place: every workgroup scans the nwg histograms itself (its own base per
+//         key: the keys before it, then the earlier chunks of the same key),
+//         then scatters its chunk; workgroup 0 writes offset[].
+// nkeys <= kSortLdsKeys, nwg <= kSortMaxChunks.
 __global__ void __launch_bounds__(1024)
-    kernel_adder_bin_scan(const int *__restrict__ count, int n,
-                          int *__restrict__ offset, int *__restrict__ cursor) {
+    kernel_home_count(const idg::Metadata *__restrict__ metadata,
+                      int nr_subgrids, int G, int S, int nr_w_layers,
+                      int chunk, int *__restrict__ hist,
+                      int2 *__restrict__ slot) {
+  extern __shared__ int lhist[];
+  const int tid = threadIdx.x;
+  const TileGrid tg(G);
+  const int nkeys = tg.nkeys(nr_w_layers);
+  for (int i = tid; i < nkeys; i += 1024) lhist[i] = 0;
+  __syncthreads();
+  const int s0 = blockIdx.x * chunk;
+  const int s1 = min(nr_subgrids, s0 + chunk);
+  // U subgrids per step, every metadata load issued before the first atomic
+  constexpr int U = 4;
+  for (int b = s0; b < s1; b += 1024 * U) {
+    int key[U];
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      const int s = b + 1024 * h + tid;
+      key[h] = s < s1 ? home_key(metadata[s], G, S, nr_w_layers, tg) : -1;
+    }
+#pragma unroll
+    for (int h = 0; h < U; ++h)
+      if (key[h] >= 0)
+        slot[b + 1024 * h + tid] = make_int2(key[h], atomicAdd(&lhist[key[h]], 1));
+  }
+  __syncthreads();
+  // key-major rows of kSortMaxChunks counts: the place kernel reads a key's
+  // row as four 16-byte loads
+  for (int i = tid; i < nkeys; i += 1024)
+    hist[static_cast<size_t>(i) * kSortMaxChunks + blockIdx.x] = lhist[i];
+}
+
+__global__ void __launch_bounds__(1024)
+    kernel_home_place(const int *__restrict__ hist, int nwg, int nkeys,
+                      int nr_subgrids, int chunk,
+                      const int2 *__restrict__ slot,
+                      int *__restrict__ offset, int *__restrict__ order) {
+  extern __shared__ int base[];  // [nkeys] bases, then [nkeys] earlier parts
+  int *pre = base + nkeys;
   __shared__ int wave_sum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, w = blockIdx.x;
+  static_assert(kSortMaxChunks == 16, "a key's row is four int4");
+  // per key: the total over the chunks and the part in earlier chunks
+#pragma unroll 4
+  for (int k = tid; k < nkeys; k += 1024) {
+    const int4 *row =
+        reinterpret_cast<const int4 *>(hist + static_cast<size_t>(k) * 16);
+    int tot = 0, p = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 v = row[q];
+      const int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 4 * q + u;
+        const int x = c < nwg ? vv[u] : 0;
+        tot += x;
+        p += c < w ? x : 0;
+      }
+    }
+    base[k] = tot;
+    pre[k] = p;
+  }
+  __syncthreads();
+  // scan of the totals over the keys (a thread takes `per` consecutive)
+  const int per = (nkeys + 1023) / 1024;
+  int t = 0;
+  for (int j = 0; j < per; ++j) {
+    const int k = tid * per + j;
+    t += k < nkeys ? base[k] : 0;
+  }
+  int e = block_scan_1024(t, wave_sum);
+  for (int j = 0; j < per; ++j) {
+    const int k = tid * per + j;
+    if (k < nkeys) {
+      const int tot = base[k];
+      if (w == 0) offset[k] = e;
+      base[k] = e + pre[k];
+      e += tot;
+    }
+  }
+  if (w == 0 && tid == 0) offset[nkeys] = nr_subgrids;
+  __syncthreads();
+  const int s0 = w * chunk, s1 = min(nr_subgrids, s0 + chunk);
+  for (int b = s0; b < s1; b += 1024 * 4) {
+    int2 k[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int s = b + 1024 * h + tid;
+      k[h] = s < s1 ? slot[s] : make_int2(-1, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      if (k[h].x >= 0) order[base[k[h].x] + k[h].y] = b + 1024 * h + tid;
+  }
+}
+
+// The same sort for more keys than LDS holds: count (pass 0) or scatter
+// (pass 1) with device-scope atomics, one thread per subgrid ...
+__global__ void __launch_bounds__(256)
+    kernel_home_key(const idg::Metadata *__restrict__ metadata,
+                    int nr_subgrids, int G, int S, int nr_w_layers, int pass,
+                    int *__restrict__ count, int *__restrict__ cursor,
+                    int *__restrict__ order) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= nr_subgrids) return;
+  const int key = home_key(metadata[s], G, S, nr_w_layers, TileGrid(G));
+  if (pass == 0)
+    atomicAdd(count + key, 1);
+  else
+    order[atomicAdd(cursor + key, 1)] = s;
+}
+
+// ... and the exclusive scan between the passes (one workgroup of 1,024, in
+// chunks of 4,096 counts): offset = cursor = the running sum, offset[n] =
+// the total.
+__global__ void __launch_bounds__(1024)
+    kernel_home_scan(const int *__restrict__ count, int n,
+                     int *__restrict__ offset, int *__restrict__ cursor) {
+  __shared__ int wave_sum[16];
+  const int tid = threadIdx.x;
   int running = 0;
   for (int base = 0; base < n; base += 4096) {
     int v[4], t = 0;
@@ -220,21 +360,10 @@ __global__ void __launch_bounds__(1024)
       v[j] = i < n ? count[i] : 0;
       t += v[j];
     }
-    int incl = t;  // inclusive scan of the thread totals within the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int o = __shfl_up(incl, d);
-      if (lane >= d) incl += o;
-    }
-    if (lane == 63) wave_sum[wave] = incl;
-    __syncthreads();
-    int before = running;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) before += w < wave ? wave_sum[w] : 0;
+    int e = running + block_scan_1024(t, wave_sum);
     int total = 0;
 #pragma unroll
     for (int w = 0; w < 16; ++w) total += wave_sum[w];
-    int e = before + incl - t;  // exclusive prefix of this thread's first
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = base + 4 * tid + j;
@@ -247,33 +376,71 @@ __global__ void __launch_bounds__(1024)
     running += total;
     __syncthreads();  // wave_sum is rewritten by the next chunk
   }
+  if (tid == 0) offset[n] = running;
 }
 
+// grid[z][pol][cy + y][cx + x] += shift_phasor(x, y) * F[s][pol][ys][xs],
+// ys = (y + S/2) % S, xs = (x + S/2) % S.
+//
+// A gather, not a scatter: one workgroup owns one TW x TH tile of one
+// w-layer, adds the pixels of the subgrids overlapping it into registers in
+// ascending subgrid order and read-modify-writes the tile once.  Every
+// subgrid pixel is read exactly once over the whole launch, there are no
+// atomics on the grid, and the summation order -- hence every bit of the
+// grid -- is deterministic.  The overlapping subgrids are gathered from the
+// home sort's ranges and sorted in LDS; a candidate list larger than the
+// LDS list falls back to an ordered scan of all the metadata, which yields
+// the same order.
 __global__ void __launch_bounds__(256)
     kernel_adder(const idg::Metadata *__restrict__ metadata, int nr_subgrids,
-                 const int *__restrict__ count, const int *__restrict__ offset,
-                 const int *__restrict__ list,
+                 const int *__restrict__ offset, const int *__restrict__ order,
                  const float2 *__restrict__ subgrids,
                  float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
-  __shared__ int keys[kAddBinCap];
-  __shared__ int2 corner[kAddBinCap];
+  // the list (subgrid ids ascending, their corners relative to the tile
+  // packed as (y - ty0 + S) << 16 | (x - tx0 + S), both in (0, S + T)) and
+  // the candidates staged for it
+  __shared__ int keys[kAddListCap], corner[kAddListCap];
+  __shared__ int cand_key[kAddListCap], cand_corner[kAddListCap];
+  __shared__ int row_begin[kAddMaxRows], row_pre[kAddMaxRows + 1];
   __shared__ int wave_count[4];
   __shared__ float2 table[kAddMaxTable];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntx = (G + kAddTile - 1) / kAddTile;
+  const TileGrid tg(G);
   // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal neighbours,
   // whose subgrid reads share cache lines, run on the same XCD's L2
   const int tl = xcd_subgrid(blockIdx.x, gridDim.x);
-  const int tx0 = (tl % ntx) * kAddTile;
-  const int ty0 = (tl / ntx) * kAddTile;
+  const int tx = tl % tg.ntx, ty = tl / tg.ntx;
+  const int tx0 = tx * kTW, ty0 = ty * kTH;
   const int z = blockIdx.y;
-  const int tile = z * ntx * ntx + tl;
   const int npix = S * S;
   const bool tabled = 2 * S - 1 <= kAddMaxTable;
   // shift phasor depends on x + y only
   if (tabled)
     for (int k = tid; k < 2 * S - 1; k += 256)
       table[k] = unit_phasor(k * (S + 1) - S, 2 * S, 1.0f);
+
+  // candidates: home tiles (tx - dx, ty - dy), dx <= DX, dy <= DY, one
+  // contiguous range of order[] per home-tile row
+  const int DX = (S - 1 + kTW - 1) / kTW, DY = (S - 1 + kTH - 1) / kTH;
+  const int nrows = min(DY, ty) + 1;
+  const int hx0 = max(0, tx - DX);
+  if (wave == 0 && nrows <= kAddMaxRows) {
+    int len = 0;
+    if (lane < nrows) {
+      const int k0 = (z * tg.nty + ty - lane) * tg.ntx;
+      const int b = offset[k0 + hx0];
+      len = offset[k0 + tx + 1] - b;
+      row_begin[lane] = b;
+    }
+    int incl = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(incl, d);
+      if (lane >= d) incl += o;
+    }
+    if (lane < nrows) row_pre[lane + 1] = incl;
+    if (lane == 0) row_pre[0] = 0;
+  }
 
   float2 acc[kAddPix][4];
 #pragma unroll
@@ -293,14 +460,15 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int h = 0; h < U; ++h) {
         const int ee = min(e + h, total - 1);
-        const int2 c = corner[ee];
+        const int2 c = make_int2(tx0 - S + (corner[ee] & 0xffff),
+                                 ty0 - S + (corner[ee] >> 16));
         const float2 *sg =
             subgrids + static_cast<size_t>(keys[ee]) * 4 * npix;
 #pragma unroll
         for (int j = 0; j < kAddPix; ++j) {
           const int i = tid + 256 * j;
-          const int x = tx0 + (i & (kAddTile - 1)) - c.x;
-          const int y = ty0 + i / kAddTile - c.y;
+          const int x = tx0 + (i & (kTW - 1)) - c.x;
+          const int y = ty0 + i / kTW - c.y;
           ok[h][j] = e + h < total && x >= 0 && x < S && y >= 0 && y < S;
           const int src =
               ok[h][j] ? half_shift(y, S) * S + half_shift(x, S) : 0;
@@ -325,29 +493,47 @@ __global__ void __launch_bounds__(256)
         }
     }
   };
+  auto pack_corner = [&](int cx, int cy) {
+    return (cy - ty0 + S) << 16 | (cx - tx0 + S);
+  };
+  auto overlaps = [&](int cx, int cy) {
+    return cx < tx0 + kTW && cx + S > tx0 && cy < ty0 + kTH && cy + S > ty0;
+  };
 
-  const int n = count[tile];
-  if (n <= kAddBinCap) {
-    // the bin sorted ascending by rank (subgrid indices are distinct): each
-    // entry's rank = the entries below it, one barrier (a bitonic sort
-    // took one per stage, 21 for a bin of 64)
-    const int off = offset[tile];
-    int *raw = reinterpret_cast<int *>(corner);  // staging, then corners
-    for (int i = tid; i < n; i += 256) raw[i] = list[off + i];
-    __syncthreads();
+  __syncthreads();
+  const int n = nrows <= kAddMaxRows ? row_pre[nrows] : kAddListCap + 1;
+  if (n <= kAddListCap) {
+    // stage the candidates (key: the id when the subgrid overlaps the
+    // tile, else kNoKey), then sort the overlapping ones ascending by rank
+    // (subgrid indices are distinct): each entry's rank = the entries below
+    // it
     for (int i = tid; i < n; i += 256) {
-      const int key = raw[i];
+      int r = 0;
+      while (row_pre[r + 1] <= i) ++r;
+      const int s = order[row_begin[r] + i - row_pre[r]];
+      const idg::Metadata m = metadata[s];
+      const int cx = m.coordinate.x, cy = m.coordinate.y;
+      cand_key[i] = overlaps(cx, cy) ? s : kNoKey;
+      cand_corner[i] = pack_corner(cx, cy);
+    }
+    __syncthreads();
+    int mine = 0;
+    for (int i = tid; i < n; i += 256) {
+      const int k = cand_key[i];
+      if (k == kNoKey) continue;
       int rank = 0;
-      for (int j = 0; j < n; ++j) rank += raw[j] < key;
-      keys[rank] = key;
+      for (int j = 0; j < n; ++j) rank += cand_key[j] < k;
+      keys[rank] = k;
+      corner[rank] = cand_corner[i];
+      ++mine;
     }
+    // the overlapping count
+    int cnt = mine;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if (lane == 0) wave_count[wave] = cnt;
     __syncthreads();
-    for (int e = tid; e < n; e += 256) {
-      const idg::Metadata m = metadata[keys[e]];
-      corner[e] = make_int2(m.coordinate.x, m.coordinate.y);
-    }
-    __syncthreads();
-    add_list(n);
+    add_list(wave_count[0] + wave_count[1] + wave_count[2] + wave_count[3]);
   } else {
     // ordered scan of all the metadata, 256 subgrids at a time
     for (int base = 0; base < nr_subgrids; base += 256) {
@@ -359,8 +545,7 @@ __global__ void __launch_bounds__(256)
         cx = m.coordinate.x;
         cy = m.coordinate.y;
         hit = fits(m, G, S, nr_w_layers) && m.coordinate.z == z &&
-              cx < tx0 + kAddTile && cx + S > tx0 && cy < ty0 + kAddTile &&
-              cy + S > ty0;
+              overlaps(cx, cy);
       }
       const unsigned long long mask = __ballot(hit);
       __syncthreads();  // the previous chunk's list is consumed
@@ -375,7 +560,7 @@ __global__ void __launch_bounds__(256)
       if (hit) {
         pos += __popcll(mask & ((1ull << lane) - 1ull));  // ordered
         keys[pos] = s;
-        corner[pos] = make_int2(cx, cy);
+        corner[pos] = pack_corner(cx, cy);
       }
       __syncthreads();
       add_list(total);
@@ -386,7 +571,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int j = 0; j < kAddPix; ++j) {
     const int i = tid + 256 * j;
-    const int gx = tx0 + (i & (kAddTile - 1)), gy = ty0 + i / kAddTile;
+    const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
     if (gx >= G || gy >= G) continue;
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol) {
@@ -396,33 +581,6 @@ __global__ void __launch_bounds__(256)
       *o = make_float2(v.x + acc[j][pol].x, v.y + acc[j][pol].y);
     }
   }
-}
-
-// The splitter's processing order: subgrids counting-sorted by the grid
-// tile holding their corner (w-layer major, then tile rows), those not
-// wholly inside the grid last.  Consecutive workgroups of one XCD
-// (xcd_subgrid) then read overlapping grid windows, which stay in that XCD's
-// L2, instead of every subgrid pulling its 32 KB window from the Infinity
-// Cache.  The order within a tile is that of the atomics; the output does
-// not depend on it (every subgrid is written by its own workgroup).
-__global__ void __launch_bounds__(256)
-    kernel_splitter_key(const idg::Metadata *__restrict__ metadata,
-                        int nr_subgrids, int G, int S, int nr_w_layers,
-                        int pass, int *__restrict__ count,
-                        int *__restrict__ cursor, int *__restrict__ order) {
-  const int s = blockIdx.x * 256 + threadIdx.x;
-  if (s >= nr_subgrids) return;
-  const idg::Metadata m = metadata[s];
-  const int ntx = (G + kAddTile - 1) / kAddTile;
-  const int key = fits(m, G, S, nr_w_layers)
-                      ? (m.coordinate.z * ntx + m.coordinate.y / kAddTile) *
-                                ntx +
-                            m.coordinate.x / kAddTile
-                      : nr_w_layers * ntx * ntx;
-  if (pass == 0)
-    atomicAdd(count + key, 1);
-  else
-    order[atomicAdd(cursor + key, 1)] = s;
 }
 
 // F[s][pol][ys][xs] = conj(shift_phasor(x, y)) * grid[z][pol][cy + y][cx + x]
@@ -721,47 +879,90 @@ hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
   return hipGetLastError();
 }
 
+namespace {
+
+// The home sort's stream-ordered workspace: hist (16 nkeys, LDS form) |
+// slot (2 ns) | offset (nkeys + 1) | order (ns) | count, cursor (nkeys each,
+// multi-kernel form).
+struct HomeSort {
+  int *ws = nullptr;
+  int *offset = nullptr, *order = nullptr;
+};
+
+hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
+                     hipStream_t stream, HomeSort *hs) {
+  const int nkeys = TileGrid(G).nkeys(W);
+  // IDG_HOME_SORT=multi forces the multi-kernel form (tests)
+  const char *form = std::getenv("IDG_HOME_SORT");
+  const bool multi = (form != nullptr && std::strcmp(form, "multi") == 0) ||
+                     nkeys > kSortLdsKeys;
+  const int nwg = std::min(kSortMaxChunks, (ns + 3071) / 3072);
+  const int chunk = (ns + nwg - 1) / nwg;
+  const size_t ints =
+      static_cast<size_t>(nkeys) + 1 + 3 * static_cast<size_t>(ns) +
+      (multi ? 2 * static_cast<size_t>(nkeys)
+             : static_cast<size_t>(kSortMaxChunks) * nkeys);
+  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&hs->ws),
+                                  ints * sizeof(int), stream);
+  if (err != hipSuccess) return err;
+  // hist rows (64 B) first, so every row and slot[] stay aligned
+  int *hist = hs->ws;
+  int2 *slot = reinterpret_cast<int2 *>(
+      hist + (multi ? 0 : static_cast<size_t>(kSortMaxChunks) * nkeys));
+  hs->offset = reinterpret_cast<int *>(slot + ns);
+  hs->order = hs->offset + nkeys + 1;
+  int *rest = hs->order + ns;
+  if (!multi) {
+    hipLaunchKernelGGL(kernel_home_count, dim3(nwg), dim3(1024),
+                       nkeys * sizeof(int), stream, md, ns, G, S, W, chunk,
+                       hist, slot);
+    hipLaunchKernelGGL(kernel_home_place, dim3(nwg), dim3(1024),
+                       2 * nkeys * sizeof(int), stream, hist, nwg, nkeys, ns,
+                       chunk, slot, hs->offset, hs->order);
+    return hipGetLastError();
+  }
+  int *count = rest, *cursor = rest + nkeys;
+  err = hipMemsetAsync(count, 0, nkeys * sizeof(int), stream);
+  if (err != hipSuccess) return err;
+  const int nb = (ns + 255) / 256;
+  hipLaunchKernelGGL(kernel_home_key, dim3(nb), dim3(256), 0, stream, md, ns,
+                     G, S, W, 0, count, cursor, hs->order);
+  hipLaunchKernelGGL(kernel_home_scan, dim3(1), dim3(1024), 0, stream, count,
+                     nkeys, hs->offset, cursor);
+  hipLaunchKernelGGL(kernel_home_key, dim3(nb), dim3(256), 0, stream, md, ns,
+                     G, S, W, 1, count, cursor, hs->order);
+  return hipGetLastError();
+}
+
+hipError_t free_home_sort(const HomeSort &hs, hipError_t err,
+                          hipStream_t stream) {
+  if (hs.ws == nullptr) return err;
+  const hipError_t ferr = hipFreeAsync(hs.ws, stream);
+  return err != hipSuccess ? err : ferr;
+}
+
+}  // namespace
+
 hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
                         int nr_w_layers, const void *d_metadata,
                         const void *d_subgrids, void *d_grid,
                         hipStream_t stream) {
   if (nr_subgrids <= 0 || nr_w_layers <= 0 || grid_size <= 0)
     return hipSuccess;
-  const int S = subgrid_size;
-  const int ntx = (grid_size + kAddTile - 1) / kAddTile;
-  const size_t ntiles = static_cast<size_t>(nr_w_layers) * ntx * ntx;
-  const int span = (S + kAddTile - 2) / kAddTile + 1;  // tiles per axis, max
-  const size_t nlist = static_cast<size_t>(nr_subgrids) * span * span;
-  // stream-ordered workspace: count | offset | cursor | list
-  int *ws = nullptr;
-  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&ws),
-                                  (3 * ntiles + nlist) * sizeof(int), stream);
-  if (err != hipSuccess) return err;
-  int *count = ws, *offset = ws + ntiles, *cursor = ws + 2 * ntiles;
-  int *list = ws + 3 * ntiles;
   const auto *md = static_cast<const idg::Metadata *>(d_metadata);
-  // one thread per (subgrid, tile of its span x span window)
-  const int nb = static_cast<int>(
-      (static_cast<long long>(nr_subgrids) * span * span + 255) / 256);
-  err = hipMemsetAsync(count, 0, ntiles * sizeof(int), stream);
+  const TileGrid tg(grid_size);
+  HomeSort hs;
+  hipError_t err = home_sort(md, nr_subgrids, grid_size, subgrid_size,
+                             nr_w_layers, stream, &hs);
   if (err == hipSuccess) {
-    hipLaunchKernelGGL(kernel_adder_bin, dim3(nb), dim3(256), 0, stream, md,
-                       nr_subgrids, grid_size, S, nr_w_layers, 0, count,
-                       cursor, list);
-    hipLaunchKernelGGL(kernel_adder_bin_scan, dim3(1), dim3(1024), 0, stream,
-                       count, static_cast<int>(ntiles), offset, cursor);
-    hipLaunchKernelGGL(kernel_adder_bin, dim3(nb), dim3(256), 0, stream, md,
-                       nr_subgrids, grid_size, S, nr_w_layers, 1, count,
-                       cursor, list);
-    hipLaunchKernelGGL(kernel_adder, dim3(ntx * ntx, nr_w_layers), dim3(256),
-                       0, stream, md, nr_subgrids, count, offset, list,
-                       static_cast<const float2 *>(d_subgrids),
-                       static_cast<float2 *>(d_grid), grid_size, S,
-                       nr_w_layers);
+    hipLaunchKernelGGL(kernel_adder, dim3(tg.ntx * tg.nty, nr_w_layers),
+                       dim3(256), 0, stream, md, nr_subgrids, hs.offset,
+                       hs.order, static_cast<const float2 *>(d_subgrids),
+                       static_cast<float2 *>(d_grid), grid_size,
+                       subgrid_size, nr_w_layers);
     err = hipGetLastError();
   }
-  const hipError_t ferr = hipFreeAsync(ws, stream);
-  return err != hipSuccess ? err : ferr;
+  return free_home_sort(hs, err, stream);
 }
 
 hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
@@ -769,45 +970,27 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
                            const void *d_grid, void *d_subgrids,
                            hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
-  const int ntx = (grid_size + kAddTile - 1) / kAddTile;
-  const int nkeys = std::max(0, nr_w_layers) * ntx * ntx + 1;
-  // stream-ordered workspace: count | offset | cursor | order
-  int *ws = nullptr;
-  hipError_t err = hipMallocAsync(
-      reinterpret_cast<void **>(&ws),
-      (3 * static_cast<size_t>(nkeys) + nr_subgrids) * sizeof(int), stream);
-  if (err != hipSuccess) return err;
-  int *count = ws, *offset = ws + nkeys, *cursor = ws + 2 * nkeys;
-  int *order = ws + 3 * nkeys;
   const auto *md = static_cast<const idg::Metadata *>(d_metadata);
-  const int nb = (nr_subgrids + 255) / 256;
-  err = hipMemsetAsync(count, 0, nkeys * sizeof(int), stream);
+  HomeSort hs;
+  hipError_t err = home_sort(md, nr_subgrids, grid_size, subgrid_size,
+                             std::max(0, nr_w_layers), stream, &hs);
   if (err == hipSuccess) {
-    hipLaunchKernelGGL(kernel_splitter_key, dim3(nb), dim3(256), 0, stream,
-                       md, nr_subgrids, grid_size, subgrid_size, nr_w_layers,
-                       0, count, cursor, order);
-    hipLaunchKernelGGL(kernel_adder_bin_scan, dim3(1), dim3(1024), 0, stream,
-                       count, nkeys, offset, cursor);
-    hipLaunchKernelGGL(kernel_splitter_key, dim3(nb), dim3(256), 0, stream,
-                       md, nr_subgrids, grid_size, subgrid_size, nr_w_layers,
-                       1, count, cursor, order);
     if (subgrid_size == 32 || subgrid_size == 64)
       hipLaunchKernelGGL(subgrid_size == 32 ? kernel_splitter_pairs<32>
                                             : kernel_splitter_pairs<64>,
-                         dim3(nr_subgrids), dim3(256), 0, stream, md, order,
-                         static_cast<const float2 *>(d_grid),
+                         dim3(nr_subgrids), dim3(256), 0, stream, md,
+                         hs.order, static_cast<const float2 *>(d_grid),
                          static_cast<float4 *>(d_subgrids), grid_size,
                          nr_w_layers);
     else
       hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0,
-                         stream, md, order,
+                         stream, md, hs.order,
                          static_cast<const float2 *>(d_grid),
                          static_cast<float2 *>(d_subgrids), grid_size,
                          subgrid_size, nr_w_layers);
     err = hipGetLastError();
   }
-  const hipError_t ferr = hipFreeAsync(ws, stream);
-  return err != hipSuccess ? err : ferr;
+  return free_home_sort(hs, err, stream);
 }
 
 }  // namespace idg_mi355x

@@ -68,8 +68,8 @@ def test_adder_matches_numpy(idg, S, G, W):
 
 
 def test_adder_crowded_tile_takes_ordered_scan(idg):
-    """More subgrids on one grid tile than the adder's LDS bin holds (2048):
-    that tile falls back to an ordered scan of the metadata; the result
+    """More candidate subgrids for one grid tile than the adder's LDS list
+    holds (2048): that tile falls back to an ordered scan of the metadata; the result
     still matches numpy and is bit-reproducible."""
     import torch
     rng = np.random.default_rng(11)
@@ -102,6 +102,39 @@ def test_splitter_matches_numpy(idg, S, G, W):
                         out, W)
     ref = pl.splitter(pl.to_complex(pl.to_pairs(g)), md, S)
     assert _rel(pl.to_complex(out.cpu().numpy()), ref) < 1e-6
+
+
+@pytest.mark.parametrize("S,G,W", [(32, 128, 1), (16, 96, 3), (64, 160, 2),
+                                   (24, 100, 2)])
+def test_home_sort_forms_agree(idg, S, G, W, monkeypatch):
+    """The adder and splitter read the subgrids counting-sorted by home tile.
+    The sort's one-workgroup LDS form and its multi-kernel form (taken when
+    the keys outgrow LDS; IDG_HOME_SORT=multi forces it) give the same grid
+    and the same subgrids, bit for bit."""
+    import torch
+    rng = np.random.default_rng(S * W + G)
+    md, sub = _random_case(rng, G, S, W, 300)
+    t_md = _md_tensor(md)
+    t_sub = torch.from_numpy(pl.to_pairs(sub)).cuda()
+    g = torch.from_numpy(pl.to_pairs(
+        rng.normal(size=(W, 4, G, G)) + 1j * rng.normal(size=(W, 4, G, G)))
+    ).cuda()
+    grids, subs = [], []
+    for form in ("lds", "multi"):
+        monkeypatch.setenv("IDG_HOME_SORT", form)
+        grid = torch.zeros((W, 4, G, G, 2), dtype=torch.float32, device="cuda")
+        idg.adder_launch(G, t_md, t_sub, grid, W)
+        out = torch.full((300, 4, S, S, 2), 7.0, dtype=torch.float32,
+                         device="cuda")
+        idg.splitter_launch(G, t_md, g, out, W)
+        torch.cuda.synchronize()
+        grids.append(grid)
+        subs.append(out)
+    assert torch.equal(grids[0], grids[1])
+    assert torch.equal(subs[0], subs[1])
+    ref = pl.adder(np.zeros((W, 4, G, G), complex), md,
+                   pl.to_complex(pl.to_pairs(sub)))
+    assert _rel(pl.to_complex(grids[0].cpu().numpy()), ref) < 1e-6
 
 
 @pytest.mark.parametrize("S", [32, 64])
