@@ -819,7 +819,7 @@ KernelChoice select_degridder(const Problem &p) {
     // the MFMA kernel has no CG
     k.func = nw8 ? IDG_PICK(4, 1, 8) : IDG_PICK(4, 1, 4);
     k.block = nw8 ? 512 : 256;
-    if (IDG_DEGRID_SPLIT && !combined_form()) {
+    if (IDG_DEGRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
       // mirror-eligible subgrids (even S only), then the others on 8-wave
       // workgroups with 1,024-pixel chunks
 #define IDG_PICK_MIRROR(NW_)                                               \

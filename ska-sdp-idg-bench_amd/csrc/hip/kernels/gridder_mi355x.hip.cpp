@@ -975,7 +975,7 @@ KernelChoice select_gridder(const Problem &p) {
       part[1] = IDG_GRIDDER_GENERAL(0);
       break;
   }
-  if (mfma && IDG_GRID_SPLIT && !combined_form()) {
+  if (mfma && IDG_GRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
     if (part[0]) k.parts[0] = {part[0], k.block, KernelChoice::kMirror};
     k.parts[1] = {part[1], k.block, KernelChoice::kGeneral};
     // no subgrid mirror-eligible: the combined kernel, one workgroup per

@@ -223,9 +223,11 @@ void print_benchmark() {
 
 namespace idg_mi355x {
 
-bool combined_form() {
+bool two_kernel_form(int nr_subgrids) {
   const char *v = std::getenv("IDG_KERNEL_FORM");
-  return v != nullptr && std::string(v) == "combined";
+  if (v != nullptr && std::string(v) == "combined") return false;
+  if (v != nullptr && std::string(v) == "split") return true;
+  return nr_subgrids >= kTwoKernelMinLaunch;
 }
 
 std::string validate(const Problem &p, const Extents &e,

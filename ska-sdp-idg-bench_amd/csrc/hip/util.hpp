@@ -139,9 +139,16 @@ struct KernelChoice {
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                         bool all_general, hipStream_t stream);
 
-// IDG_KERNEL_FORM=combined: the device entries launch the one combined
-// kernel instead of the two-kernel form (A/B and tests; read per call).
-bool combined_form();
+// Whether the device entries launch the two-kernel form (mirror kernel +
+// queue-fed general kernel) or the one combined kernel: the two-kernel form
+// from kTwoKernelMinLaunch subgrids up.  Below that (the N >= 4 shards of
+// the batch) its fixed cost -- the queue's allocation and clear and a second
+// launch, ~15 us per direction -- outweighs what the mirror kernel's own
+// register allocation saves (one-GPU shard rehearsal at N = 8: 0.953 with
+// it, 0.969 without).  IDG_KERNEL_FORM=combined / split forces either (A/B
+// and tests; read per call).
+constexpr int kTwoKernelMinLaunch = 8192;
+bool two_kernel_form(int nr_subgrids);
 
 // Defined in the kernel TUs.
 KernelChoice select_gridder(const Problem &p);

@@ -209,9 +209,14 @@ def test_gridder_fill_scale_paths_vs_oracle(idg, oracle_lib, pattern):
         assert _rel_rms(g[s], go[s]) <= TOLERANCE, (pattern, s)
 
 
-def test_mixed_mirror_and_general_subgrids_in_one_launch(idg, oracle_lib):
+@pytest.mark.parametrize("form", ["split", "combined"])
+def test_mixed_mirror_and_general_subgrids_in_one_launch(idg, oracle_lib,
+                                                         form, monkeypatch):
     # w = 0 subgrids (mirror GEMMs) next to w != 0 subgrids (single-pixel
-    # GEMMs) in the same launch; W_STEP = 0 so only w decides
+    # GEMMs) in the same launch; W_STEP = 0 so only w decides.  A batch this
+    # small takes the combined kernel by default (util.hpp:
+    # kTwoKernelMinLaunch); both forms are checked
+    monkeypatch.setenv("IDG_KERNEL_FORM", form)
     st, ts, T, C, G, S = 4, 2, 16, 8, 512, 32
     a = idg.generate(st, ts, T, C, G, S)
     md = a["metadata"]
@@ -855,3 +860,4 @@ def test_two_kernel_launch_matches_combined_kernel(idg, full, full_w,
         diff = (two.double() - one.double()).reshape(ns, -1).abs().amax(1)
         mag = one.double().reshape(ns, -1).abs().amax(1)
         assert float((diff / mag).max()) <= TOLERANCE
+
