@@ -476,6 +476,10 @@ __device__ __forceinline__ void degrid_mfma(
 
 }  // namespace
 
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+__device__ WgStamp idg_debug_timeline_degridder[kTimelineMax];
+#endif
+
 // CG: channels per lane (VALU paths).
 // MODE: 0 = VALU kernel, 1 = MFMA kernel (mirror GEMMs on eligible
 //       subgrids, single-pixel GEMMs with the w-term on the others).
@@ -524,6 +528,9 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
     __syncthreads();
     const bool eligible = lds[0] == 0u && S % 2 == 0 && g.w_offset == 0.0f;
     __syncthreads();
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+    timeline_start(idg_debug_timeline_degridder);
+#endif
     if (eligible)
       degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
@@ -532,6 +539,9 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
       degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
           visibilities, spheroidal, aterms, sg, lds);
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+    timeline_end(idg_debug_timeline_degridder);
+#endif
     return;
   }
 
@@ -889,3 +899,13 @@ void c_run_degridder(
 }
 
 }  // namespace hip
+
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+// Debug builds only: the last combined-degridder launch's workgroup stamps
+// (tests/debug/wg_timeline.py).
+extern "C" int idg_debug_timeline_degridder_copy(void *host, int n) {
+  return hipMemcpyFromSymbol(
+      host, HIP_SYMBOL(idg_mi355x::idg_debug_timeline_degridder),
+      sizeof(WgStamp) * std::min(n, kTimelineMax));
+}
+#endif

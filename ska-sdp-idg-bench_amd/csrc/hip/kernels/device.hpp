@@ -233,3 +233,29 @@ __device__ __forceinline__ void load_jones(const float4 *p, idg::cfloat *j) {
 }
 
 }  // namespace idg_mi355x
+
+// Debug builds only (-DIDG_WG_TIMELINE=1, tests/debug/wg_timeline.py): per
+// workgroup wall-clock start / end (s_memrealtime, 100 MHz), HW_ID and
+// XCC_ID of the combined kernels, written by thread 0 with vector stores.
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+constexpr int kTimelineMax = 32768;
+struct WgStamp {
+  unsigned long long t0, t1;
+  unsigned hw_id, xcc_id;
+};
+__device__ __forceinline__ void timeline_start(WgStamp *tl) {
+  if (threadIdx.x == 0 && blockIdx.x < kTimelineMax) {
+    WgStamp w;
+    w.t0 = static_cast<unsigned long long>(wall_clock64());
+    w.t1 = 0;
+    w.hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    w.xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    tl[blockIdx.x] = w;
+  }
+}
+__device__ __forceinline__ void timeline_end(WgStamp *tl) {
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < kTimelineMax)
+    tl[blockIdx.x].t1 = static_cast<unsigned long long>(wall_clock64());
+}
+#endif

@@ -705,6 +705,10 @@ __device__ __forceinline__ void grid_mfma(
 
 }  // namespace
 
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+__device__ WgStamp idg_debug_timeline_gridder[kTimelineMax];
+#endif
+
 // S_CT: subgrid size known at compile time (0 = runtime).
 // PPT : pixels per lane (VALU paths).   CB: channels per phase anchor.
 // MODE: 0 = VALU kernel (VALU mirror path + general path, every subgrid),
@@ -750,6 +754,9 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
     constexpr int NW = IDG_GRID_NW;
     // both paths hold 2 PT accumulator tiles per wave
     __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+    timeline_start(idg_debug_timeline_gridder);
+#endif
     if (mirror)
       grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
                                         nr_stations, uvw, wavenumbers,
@@ -759,6 +766,9 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
       grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
           visibilities, spheroidal, aterms, out, lds);
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+    timeline_end(idg_debug_timeline_gridder);
+#endif
     return;
   }
 
@@ -1017,3 +1027,13 @@ void c_run_gridder(
 }
 
 }  // namespace hip
+
+#if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
+// Debug builds only: the last combined-gridder launch's workgroup stamps
+// (tests/debug/wg_timeline.py).
+extern "C" int idg_debug_timeline_gridder_copy(void *host, int n) {
+  return hipMemcpyFromSymbol(
+      host, HIP_SYMBOL(idg_mi355x::idg_debug_timeline_gridder),
+      sizeof(WgStamp) * std::min(n, kTimelineMax));
+}
+#endif
