@@ -147,7 +147,8 @@ __global__ void __launch_bounds__(256)
 // The home sort: subgrids counting-sorted by their home tile, the grid tile
 // (TW x TH, w-layer major, then tile rows) holding their corner, with the
 // subgrids not wholly inside the grid last.  offset[key] is the first
-// position of key's subgrids in order[], offset[nkeys] = nr_subgrids.  Both
+// position of key's subgrids in order[] (entries {s, x, y, z}, z = -1 when
+// not wholly inside the grid), offset[nkeys] = nr_subgrids.  Both
 // the adder and the splitter read it:
 //  * the adder's tile finds the subgrids overlapping it in the home tiles up
 //    to ceil((S - 1) / TW) tiles left and ceil((S - 1) / TH) tiles up of
@@ -222,17 +223,20 @@ __device__ __forceinline__ int block_scan_1024(int t, int *wave_sum) {
 // owning a contiguous chunk of subgrids, with its counters in LDS (no
 // device-scope atomics, which cross the XCDs: a counting pass of 24,500 of
 // them took 19 us; one workgroup sorting everything took 47 us):
-//  count: key and rank within the chunk's home tile -> slot[s], the chunk's
-//         histogram -> hist[key][w];
+//  count: key, rank within the chunk's home tile and corner -> slot[s], the
+//         chunk's histogram -> hist[key][w];
 //  place: every workgroup scans the nwg histograms itself (its own base per
 //         key: the keys before it, then the earlier chunks of the same key),
-//         then scatters its chunk; workgroup 0 writes offset[].
+//         then scatters its chunk as entries {s, x, y, z} (z = -1: not
+//         wholly inside the grid), so the adder and splitter read a
+//         subgrid's corner with its index, not through its metadata;
+//         workgroup 0 writes offset[].
 // nkeys <= kSortLdsKeys, nwg <= kSortMaxChunks.
 __global__ void __launch_bounds__(1024)
     kernel_home_count(const idg::Metadata *__restrict__ metadata,
                       int nr_subgrids, int G, int S, int nr_w_layers,
                       int chunk, int *__restrict__ hist,
-                      int2 *__restrict__ slot) {
+                      int4 *__restrict__ slot) {
   extern __shared__ int lhist[];
   const int tid = threadIdx.x;
   const TileGrid tg(G);
@@ -244,16 +248,23 @@ __global__ void __launch_bounds__(1024)
   // U subgrids per step, every metadata load issued before the first atomic
   constexpr int U = 4;
   for (int b = s0; b < s1; b += 1024 * U) {
-    int key[U];
+    int key[U], cx[U], cy[U];
 #pragma unroll
     for (int h = 0; h < U; ++h) {
       const int s = b + 1024 * h + tid;
-      key[h] = s < s1 ? home_key(metadata[s], G, S, nr_w_layers, tg) : -1;
+      key[h] = -1;
+      if (s < s1) {
+        const idg::Metadata m = metadata[s];
+        key[h] = home_key(m, G, S, nr_w_layers, tg);
+        cx[h] = m.coordinate.x;
+        cy[h] = m.coordinate.y;
+      }
     }
 #pragma unroll
     for (int h = 0; h < U; ++h)
       if (key[h] >= 0)
-        slot[b + 1024 * h + tid] = make_int2(key[h], atomicAdd(&lhist[key[h]], 1));
+        slot[b + 1024 * h + tid] =
+            make_int4(key[h], atomicAdd(&lhist[key[h]], 1), cx[h], cy[h]);
   }
   __syncthreads();
   // key-major rows of kSortMaxChunks counts: the place kernel reads a key's
@@ -264,9 +275,9 @@ __global__ void __launch_bounds__(1024)
 
 __global__ void __launch_bounds__(1024)
     kernel_home_place(const int *__restrict__ hist, int nwg, int nkeys,
-                      int nr_subgrids, int chunk,
-                      const int2 *__restrict__ slot,
-                      int *__restrict__ offset, int *__restrict__ order) {
+                      int keys_per_layer, int nr_subgrids, int chunk,
+                      const int4 *__restrict__ slot,
+                      int *__restrict__ offset, int4 *__restrict__ order) {
   extern __shared__ int base[];  // [nkeys] bases, then [nkeys] earlier parts
   int *pre = base + nkeys;
   __shared__ int wave_sum[16];
@@ -315,15 +326,18 @@ __global__ void __launch_bounds__(1024)
   __syncthreads();
   const int s0 = w * chunk, s1 = min(nr_subgrids, s0 + chunk);
   for (int b = s0; b < s1; b += 1024 * 4) {
-    int2 k[4];
+    int4 k[4];
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const int s = b + 1024 * h + tid;
-      k[h] = s < s1 ? slot[s] : make_int2(-1, 0);
+      k[h] = s < s1 ? slot[s] : make_int4(-1, 0, 0, 0);
     }
 #pragma unroll
     for (int h = 0; h < 4; ++h)
-      if (k[h].x >= 0) order[base[k[h].x] + k[h].y] = b + 1024 * h + tid;
+      if (k[h].x >= 0)
+        order[base[k[h].x] + k[h].y] = make_int4(
+            b + 1024 * h + tid, k[h].z, k[h].w,
+            k[h].x < nkeys - 1 ? k[h].x / keys_per_layer : -1);
   }
 }
 
@@ -333,14 +347,17 @@ __global__ void __launch_bounds__(256)
     kernel_home_key(const idg::Metadata *__restrict__ metadata,
                     int nr_subgrids, int G, int S, int nr_w_layers, int pass,
                     int *__restrict__ count, int *__restrict__ cursor,
-                    int *__restrict__ order) {
+                    int4 *__restrict__ order) {
   const int s = blockIdx.x * 256 + threadIdx.x;
   if (s >= nr_subgrids) return;
-  const int key = home_key(metadata[s], G, S, nr_w_layers, TileGrid(G));
+  const idg::Metadata m = metadata[s];
+  const int key = home_key(m, G, S, nr_w_layers, TileGrid(G));
   if (pass == 0)
     atomicAdd(count + key, 1);
   else
-    order[atomicAdd(cursor + key, 1)] = s;
+    order[atomicAdd(cursor + key, 1)] =
+        make_int4(s, m.coordinate.x, m.coordinate.y,
+                  fits(m, G, S, nr_w_layers) ? m.coordinate.z : -1);
 }
 
 // ... and the exclusive scan between the passes (one workgroup of 1,024, in
@@ -393,7 +410,7 @@ __global__ void __launch_bounds__(1024)
 // the same order.
 __global__ void __launch_bounds__(256)
     kernel_adder(const idg::Metadata *__restrict__ metadata, int nr_subgrids,
-                 const int *__restrict__ offset, const int *__restrict__ order,
+                 const int *__restrict__ offset, const int4 *__restrict__ order,
                  const float2 *__restrict__ subgrids,
                  float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
   // the list (subgrid ids ascending, their corners relative to the tile
@@ -510,10 +527,9 @@ __global__ void __launch_bounds__(256)
     for (int i = tid; i < n; i += 256) {
       int r = 0;
       while (row_pre[r + 1] <= i) ++r;
-      const int s = order[row_begin[r] + i - row_pre[r]];
-      const idg::Metadata m = metadata[s];
-      const int cx = m.coordinate.x, cy = m.coordinate.y;
-      cand_key[i] = overlaps(cx, cy) ? s : kNoKey;
+      const int4 e = order[row_begin[r] + i - row_pre[r]];  // {s, x, y, z}
+      const int cx = e.y, cy = e.z;
+      cand_key[i] = overlaps(cx, cy) ? e.x : kNoKey;
       cand_corner[i] = pack_corner(cx, cy);
     }
     __syncthreads();
@@ -586,20 +602,19 @@ __global__ void __launch_bounds__(256)
 // F[s][pol][ys][xs] = conj(shift_phasor(x, y)) * grid[z][pol][cy + y][cx + x]
 // (zero when the subgrid does not lie inside the grid).
 __global__ void __launch_bounds__(256)
-    kernel_splitter(const idg::Metadata *__restrict__ metadata,
-                    const int *__restrict__ order,
+    kernel_splitter(const int4 *__restrict__ order,
                     const float2 *__restrict__ grid,
-                    float2 *__restrict__ subgrids, int G, int S,
-                    int nr_w_layers) {
+                    float2 *__restrict__ subgrids, int G, int S) {
   __shared__ float2 table[kAddMaxTable];
-  const int s = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  // the home sort's entry {s, x, y, z}, z = -1 when not inside the grid
+  const int4 e = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  const int s = e.x;
   const int tid = threadIdx.x, nt = blockDim.x;
-  const idg::Metadata m = metadata[s];
-  const bool inside = fits(m, G, S, nr_w_layers);
+  const bool inside = e.w >= 0;
   const int npix = S * S;
   float2 *sg = subgrids + static_cast<size_t>(s) * 4 * npix;
   const float2 *gz =
-      grid + static_cast<size_t>(inside ? m.coordinate.z : 0) * 4 * G * G;
+      grid + static_cast<size_t>(inside ? e.w : 0) * 4 * G * G;
   // the shift phasor depends on x + y only: 2S - 1 values per subgrid
   const bool tabled = 2 * S - 1 <= kAddMaxTable;
   if (tabled)
@@ -613,7 +628,7 @@ __global__ void __launch_bounds__(256)
     const int dst = half_shift(y, S) * S + half_shift(x, S);
     const float2 ph = tabled ? table[x + y] : shift_phasor(x, y, S, -1.0f);
     const size_t src =
-        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+        static_cast<size_t>(e.z + y) * G + e.y + x;
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol)
       store_stream(&sg[pol * npix + dst],
@@ -635,19 +650,18 @@ __global__ void __launch_bounds__(256)
 // before its first store.  The same arithmetic as kernel_splitter.
 template <int S>
 __global__ void __launch_bounds__(256)
-    kernel_splitter_pairs(const idg::Metadata *__restrict__ metadata,
-                          const int *__restrict__ order,
+    kernel_splitter_pairs(const int4 *__restrict__ order,
                           const float2 *__restrict__ grid,
-                          float4 *__restrict__ subgrids, int G,
-                          int nr_w_layers) {
+                          float4 *__restrict__ subgrids, int G) {
   static_assert(S % 4 == 0 && (S * S / 2) % 256 == 0, "whole pair rows");
   constexpr int PR = S * S / 2 / 256;  // pairs per thread
   constexpr int npix = S * S;
   __shared__ float2 table[2 * S - 1];
-  const int s = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  // the home sort's entry {s, x, y, z}, z = -1 when not inside the grid
+  const int4 e = order[xcd_subgrid(blockIdx.x, gridDim.x)];
+  const int s = e.x;
   const int tid = threadIdx.x;
-  const idg::Metadata m = metadata[s];
-  const bool inside = fits(m, G, S, nr_w_layers);
+  const bool inside = e.w >= 0;
   for (int k = tid; k < 2 * S - 1; k += 256)
     table[k] = unit_phasor(k * (S + 1) - S, 2 * S, -1.0f);
   __syncthreads();
@@ -661,14 +675,14 @@ __global__ void __launch_bounds__(256)
                      make_float4(0.f, 0.f, 0.f, 0.f));
     return;
   }
-  const float2 *gz = grid + static_cast<size_t>(m.coordinate.z) * 4 * G * G;
+  const float2 *gz = grid + static_cast<size_t>(e.w) * 4 * G * G;
   float2 v[PR][4][2];
 #pragma unroll
   for (int j = 0; j < PR; ++j) {
     const int p = tid + 256 * j;
     const int y = p / (S / 2), x = 2 * (p % (S / 2));
     const size_t src =
-        static_cast<size_t>(m.coordinate.y + y) * G + m.coordinate.x + x;
+        static_cast<size_t>(e.z + y) * G + e.y + x;
 #pragma unroll
     for (int pol = 0; pol < 4; ++pol) {
       v[j][pol][0] = gz[static_cast<size_t>(pol) * G * G + src];
@@ -886,12 +900,14 @@ namespace {
 // multi-kernel form).
 struct HomeSort {
   int *ws = nullptr;
-  int *offset = nullptr, *order = nullptr;
+  int *offset = nullptr;
+  int4 *order = nullptr;  // entries {s, x, y, z or -1}
 };
 
 hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
                      hipStream_t stream, HomeSort *hs) {
-  const int nkeys = TileGrid(G).nkeys(W);
+  const TileGrid tg(G);
+  const int nkeys = tg.nkeys(W);
   // IDG_HOME_SORT=multi forces the multi-kernel form (tests)
   const char *form = std::getenv("IDG_HOME_SORT");
   const bool multi = (form != nullptr && std::strcmp(form, "multi") == 0) ||
@@ -899,26 +915,27 @@ hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
   const int nwg = std::min(kSortMaxChunks, (ns + 3071) / 3072);
   const int chunk = (ns + nwg - 1) / nwg;
   const size_t ints =
-      static_cast<size_t>(nkeys) + 1 + 3 * static_cast<size_t>(ns) +
+      static_cast<size_t>(nkeys) + 1 + 8 * static_cast<size_t>(ns) +
       (multi ? 2 * static_cast<size_t>(nkeys)
              : static_cast<size_t>(kSortMaxChunks) * nkeys);
   hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&hs->ws),
                                   ints * sizeof(int), stream);
   if (err != hipSuccess) return err;
-  // hist rows (64 B) first, so every row and slot[] stay aligned
+  // hist rows (64 B) first, then the 16-byte slot[] and order[] entries
   int *hist = hs->ws;
-  int2 *slot = reinterpret_cast<int2 *>(
+  int4 *slot = reinterpret_cast<int4 *>(
       hist + (multi ? 0 : static_cast<size_t>(kSortMaxChunks) * nkeys));
-  hs->offset = reinterpret_cast<int *>(slot + ns);
-  hs->order = hs->offset + nkeys + 1;
-  int *rest = hs->order + ns;
+  hs->order = slot + ns;
+  hs->offset = reinterpret_cast<int *>(hs->order + ns);
+  int *rest = hs->offset + nkeys + 1;
   if (!multi) {
     hipLaunchKernelGGL(kernel_home_count, dim3(nwg), dim3(1024),
                        nkeys * sizeof(int), stream, md, ns, G, S, W, chunk,
                        hist, slot);
     hipLaunchKernelGGL(kernel_home_place, dim3(nwg), dim3(1024),
-                       2 * nkeys * sizeof(int), stream, hist, nwg, nkeys, ns,
-                       chunk, slot, hs->offset, hs->order);
+                       2 * nkeys * sizeof(int), stream, hist, nwg, nkeys,
+                       tg.ntx * tg.nty, ns, chunk, slot, hs->offset,
+                       hs->order);
     return hipGetLastError();
   }
   int *count = rest, *cursor = rest + nkeys;
@@ -978,16 +995,15 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
     if (subgrid_size == 32 || subgrid_size == 64)
       hipLaunchKernelGGL(subgrid_size == 32 ? kernel_splitter_pairs<32>
                                             : kernel_splitter_pairs<64>,
-                         dim3(nr_subgrids), dim3(256), 0, stream, md,
-                         hs.order, static_cast<const float2 *>(d_grid),
-                         static_cast<float4 *>(d_subgrids), grid_size,
-                         nr_w_layers);
+                         dim3(nr_subgrids), dim3(256), 0, stream, hs.order,
+                         static_cast<const float2 *>(d_grid),
+                         static_cast<float4 *>(d_subgrids), grid_size);
     else
       hipLaunchKernelGGL(kernel_splitter, dim3(nr_subgrids), dim3(256), 0,
-                         stream, md, hs.order,
+                         stream, hs.order,
                          static_cast<const float2 *>(d_grid),
                          static_cast<float2 *>(d_subgrids), grid_size,
-                         subgrid_size, nr_w_layers);
+                         subgrid_size);
     err = hipGetLastError();
   }
   return free_home_sort(hs, err, stream);
