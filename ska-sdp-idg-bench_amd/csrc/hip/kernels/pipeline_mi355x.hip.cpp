@@ -169,6 +169,9 @@ __global__ void __launch_bounds__(256)
 #ifndef IDG_ADD_U
 #define IDG_ADD_U 4
 #endif
+#ifndef IDG_ADD_MASKED
+#define IDG_ADD_MASKED 1
+#endif
 constexpr int kTW = IDG_ADD_TW;  // grid tile width (pixels)
 constexpr int kTH = IDG_ADD_TH;  // grid tile height
 constexpr int kAddPix = kTW * kTH / 256;  // tile pixels per thread
@@ -492,8 +495,20 @@ __global__ void __launch_bounds__(256)
           ph[h][j] = !ok[h][j] ? make_float2(0.0f, 0.0f)
                      : tabled  ? table[x + y]
                                : shift_phasor(x, y, S, 1.0f);
+#if IDG_ADD_MASKED
+          // lanes outside the entry's subgrid issue no load (a wave with
+          // none inside skips the entry's loads)
+          if (ok[h][j]) {
+#pragma unroll
+            for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = sg[pol * npix + src];
+          } else {
+#pragma unroll
+            for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = make_float2(0.f, 0.f);
+          }
+#else
 #pragma unroll
           for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = sg[pol * npix + src];
+#endif
         }
       }
 #pragma unroll
