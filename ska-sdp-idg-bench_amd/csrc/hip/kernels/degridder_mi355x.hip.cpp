@@ -820,7 +820,10 @@ KernelChoice select_degridder(const Problem &p) {
   // the last round (0.926 vs 0.935 ms at 3,063 subgrids); large ones keep
   // 4 waves (7.18 vs 7.21-7.26 ms at 24,500).  Same
   // arithmetic, bitwise identical outputs.
-  const bool nw8 = mfma && p.nr_subgrids < kDegridSmallLaunch;
+  bool nw8 = mfma && p.nr_subgrids < kDegridSmallLaunch;
+  // IDG_DEGRID_NW=4 / 8 forces the workgroup size (tests; read per call)
+  if (const char *v = std::getenv("IDG_DEGRID_NW"))
+    nw8 = mfma && std::string(v) == "8";
 #define IDG_PICK(CG_, MODE_, NW_)                                          \
   (s32 ? IDG_DEGRIDDER(32, CG_, MODE_, NW_)                                \
        : (s64 ? IDG_DEGRIDDER(64, CG_, MODE_, NW_)                         \

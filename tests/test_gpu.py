@@ -861,3 +861,37 @@ def test_two_kernel_launch_matches_combined_kernel(idg, full, full_w,
         mag = one.double().reshape(ns, -1).abs().amax(1)
         assert float((diff / mag).max()) <= TOLERANCE
 
+
+
+@pytest.mark.parametrize("form", ["combined", "split"])
+def test_degridder_4_and_8_wave_workgroups_bitwise_on_ragged_batches(
+        idg, form, monkeypatch):
+    """Launches below 4,096 subgrids degrid on 8-wave workgroups (128
+    timesteps per pass), larger ones on 4-wave ones (64).  Timestep counts
+    that fill neither pass (ragged rows take the partial-tile store path)
+    and w != 0 on some subgrids: IDG_DEGRID_NW=4 and =8 give the same
+    visibilities bit for bit, in both launch forms."""
+    import torch
+    st, ts, T, C, G, S = 6, 3, 100, 20, 512, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    md = a["metadata"].copy()
+    rng = np.random.default_rng(17)
+    md["nr_timesteps"] = rng.integers(0, T + 1, md.size)
+    a["uvw"][1::4, :, 2] = rng.uniform(-100.0, 100.0,
+                                       a["uvw"][1::4, :, 2].shape)
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    dev = _to_device(dict(a, metadata=md))
+    monkeypatch.setenv("IDG_KERNEL_FORM", form)
+    outs = []
+    for nw in ("4", "8"):
+        monkeypatch.setenv("IDG_DEGRID_NW", nw)
+        out = torch.full_like(dev["visibilities"], 7.25)
+        idg.degridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], out,
+                             dev["spheroidal"], dev["aterms"],
+                             dev["metadata"], dev["subgrids"])
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0] != 7.25).any()
