@@ -585,8 +585,9 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
     nw = w.get("w_layers", 1)
     gridt = torch.zeros((nw, 4, G, G, 2), dtype=torch.float32, device="cuda")
     uvsub = torch.empty_like(sub_out)
+    uvfused = torch.empty_like(sub_out)
     npipe = max(1, min(steps, 5))
-    pev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    pev = [[torch.cuda.Event(enable_timing=True) for _ in range(7)]
            for _ in range(npipe)]
     has = sub_out.shape[0] > 0
     for it in range(npipe + 1):
@@ -618,6 +619,13 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
                                        stream=stream)
         if e:
             e[5].record(stream)
+        # the same two steps as one fused kernel (S = 32 / 64), into a
+        # buffer of its own
+        if has:
+            idg_amd.splitter_fft_launch(G, dev["metadata"], gridt, uvfused,
+                                        nr_w_layers=nw, stream=stream)
+        if e:
+            e[6].record(stream)
     torch.cuda.synchronize()
 
     def avg(i, j):
@@ -629,6 +637,10 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
         "grid_reduce_ms": round(avg(2, 3), 4),
         "splitter_ms": round(avg(3, 4), 4),
         "ifft_ms": round(avg(4, 5), 4),
+        "splitter_fft_ms": round(avg(5, 6), 4),
+        "splitter_fft": ("splitter + inverse FFT fused "
+                         "(idg_splitter_fft_launch), bit for bit "
+                         "splitter_ms + ifft_ms's output"),
         "grid": (f"[{nw}][4][{G}][{G}] complex64, "
                  f"{nw * G * G * 32 / 2**20:.0f} MiB"),
         "grid_reduce": (f"all_reduce(sum) of the ranks' partial grids, "
@@ -640,7 +652,8 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
     sub_b = sub_out.numel() * 4
     grid_b = gridt.numel() * 4
     algo = {"fft_ms": 2 * sub_b, "adder_ms": sub_b + 2 * grid_b,
-            "splitter_ms": sub_b + grid_b, "ifft_ms": 2 * sub_b}
+            "splitter_ms": sub_b + grid_b, "ifft_ms": 2 * sub_b,
+            "splitter_fft_ms": sub_b + grid_b}
     roof = {}
     for k, nbytes in algo.items():
         t = out[k] / 1e3

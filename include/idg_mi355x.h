@@ -204,6 +204,15 @@ int idg_splitter_launch(int nr_subgrids, int grid_size, int subgrid_size,
                         const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
                         void *stream);
 
+/* idg_splitter_launch followed by idg_subgrid_fft_launch(-1, 1/S^2): the
+ * degridder's input subgrids straight from the grid.  For S = 32 and 64 one
+ * fused kernel (the uv-domain subgrids never reach HBM), bit for bit the
+ * two launches' result; other even S <= 64 run the two launches. */
+int idg_splitter_fft_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                            int nr_w_layers, const idg_metadata_t *metadata,
+                            const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
+                            void *stream);
+
 /* ---- synthetic observation (app/common/init.cpp:4-180) -------------------
  * Exactly the reference harness' inputs: srand(0), then the initialize_*
  * generators in harness order.  nr_subgrids = nr_stations*(nr_stations-1)/2

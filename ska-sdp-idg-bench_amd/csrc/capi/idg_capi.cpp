@@ -141,6 +141,22 @@ int idg_splitter_launch(int nr_subgrids, int grid_size, int subgrid_size,
                   "idg_splitter_launch");
 }
 
+int idg_splitter_fft_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                            int nr_w_layers, const idg_metadata_t *metadata,
+                            const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
+                            void *stream) {
+  if (nr_subgrids < 0 || subgrid_size <= 0 || subgrid_size % 2 ||
+      subgrid_size > 64 || grid_size < subgrid_size || nr_w_layers <= 0)
+    return fail(IDG_E_INVALID_ARGUMENT,
+                "even subgrid_size <= min(64, grid_size), nr_w_layers > 0 "
+                "required");
+  return from_hip(idg_mi355x::launch_splitter_fft(
+                      nr_subgrids, grid_size, subgrid_size, nr_w_layers,
+                      metadata, grid, subgrids,
+                      static_cast<hipStream_t>(stream)),
+                  "idg_splitter_fft_launch");
+}
+
 int idg_c_run_gridder(int nr_subgrids, int grid_size, int subgrid_size,
                       float image_size, float w_step_in_lambda,
                       int nr_channels, int nr_stations, const idg_uvw_t *uvw,

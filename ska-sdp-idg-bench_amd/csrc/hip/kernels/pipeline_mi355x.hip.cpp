@@ -870,6 +870,85 @@ __global__ void __launch_bounds__(128)
   }
 }
 
+// The splitter and the degridding FFT (sign -1, scale 1/S^2) in one pass,
+// for S = 32 / 64: the uv-domain subgrid never goes to HBM.  A workgroup of
+// 128 threads takes P = 128 / N correlation planes of one subgrid (a whole
+// S = 32 subgrid, half an S = 64 one), in the home sort's order
+// (xcd_subgrid: consecutive workgroups of one XCD read overlapping grid
+// windows from its L2).  Every thread keeps one window column x (128 is a
+// multiple of N), so each wave-load reads whole grid-row segments; the
+// splitter's value cmulf(conj shift phasor, grid) goes straight to its
+// fftshifted place in the padded LDS planes, and the rest is
+// kernel_subgrid_fft_reg's transform: the same operations in the same order
+// as kernel_splitter_pairs followed by kernel_subgrid_fft_reg, so the output
+// is bit for bit theirs.  A subgrid not wholly inside the grid transforms
+// zeros, as the two-kernel path does.
+template <int N>
+__global__ void __launch_bounds__(128)
+    kernel_splitter_fft(const int4 *__restrict__ order,
+                        const float2 *__restrict__ grid,
+                        float2 *__restrict__ subgrids, int G, float sign,
+                        float scale) {
+  constexpr int P = 128 / N;   // planes per workgroup
+  constexpr int WPS = 4 / P;   // workgroups per subgrid
+  constexpr int RS = N + 1;    // padded LDS row stride (complex)
+  constexpr int K = P * N * N / 128;  // window values per thread
+  __shared__ float2 lds[P * N * RS];
+  __shared__ float2 table[2 * N - 1];
+  const int tid = threadIdx.x;
+  const int b = xcd_subgrid(blockIdx.x, gridDim.x);
+  // the home sort's entry {s, x, y, z}, z = -1 when not inside the grid
+  const int4 e = order[b / WPS];
+  const int pol0 = (b % WPS) * P;
+  const bool inside = e.w >= 0;
+  for (int k = tid; k < 2 * N - 1; k += 128)
+    table[k] = unit_phasor(k * (N + 1) - N, 2 * N, -1.0f);
+  const int x = tid % N, y0 = tid / N;
+  const float2 *gz =
+      grid + (static_cast<size_t>(inside ? e.w : 0) * 4 + pol0) * G * G +
+      static_cast<size_t>(inside ? e.z : 0) * G + (inside ? e.y : 0) + x;
+  // every grid load of the thread in flight before the first LDS write
+  float2 v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = y0 + P * k;  // plane-major rows: plane r / N, row r % N
+    v[k] = inside ? gz[static_cast<size_t>(r / N) * G * G +
+                       static_cast<size_t>(r % N) * G]
+                  : make_float2(0.0f, 0.0f);
+  }
+  float2 tw[N / 2];
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) tw[k] = unit_phasor(k, N, sign);
+  __syncthreads();  // table
+  const int xs = half_shift(x, N);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = y0 + P * k, pp = r / N, y = r % N;
+    lds[pp * N * RS + half_shift(y, N) * RS + xs] =
+        inside ? cmulf(table[x + y], v[k]) : v[k];
+  }
+  __syncthreads();
+
+  const int p = tid / N, q = tid % N;  // plane, row (then column)
+  float2 f[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) f[i] = lds[p * N * RS + q * RS + i];
+  fft_dif_registers<N>(f, tw);
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    lds[p * N * RS + q * RS + bit_reverse<N>(i)] = f[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) f[i] = lds[p * N * RS + i * RS + q];
+  fft_dif_registers<N>(f, tw);
+  float2 *out =
+      subgrids + (static_cast<size_t>(e.x) * 4 + pol0 + p) * N * N;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    store_stream(&out[bit_reverse<N>(i) * N + q],
+                 make_float2(f[i].x * scale, f[i].y * scale));
+}
+
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
                               float scale, void *d_subgrids,
                               hipStream_t stream) {
@@ -1019,6 +1098,39 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
                          static_cast<const float2 *>(d_grid),
                          static_cast<float2 *>(d_subgrids), grid_size,
                          subgrid_size);
+    err = hipGetLastError();
+  }
+  return free_home_sort(hs, err, stream);
+}
+
+hipError_t launch_splitter_fft(int nr_subgrids, int grid_size,
+                               int subgrid_size, int nr_w_layers,
+                               const void *d_metadata, const void *d_grid,
+                               void *d_subgrids, hipStream_t stream) {
+  if (nr_subgrids <= 0) return hipSuccess;
+  const int S = subgrid_size;
+  const float scale = 1.0f / static_cast<float>(S * S);
+  // IDG_SPLIT_FFT=0: the two launches (A/B and tests)
+  const char *env = std::getenv("IDG_SPLIT_FFT");
+  if ((S != 32 && S != 64) || (env != nullptr && env[0] == '0')) {
+    const hipError_t err =
+        launch_splitter(nr_subgrids, grid_size, S, nr_w_layers, d_metadata,
+                        d_grid, d_subgrids, stream);
+    if (err != hipSuccess) return err;
+    return launch_subgrid_fft(nr_subgrids, S, -1, scale, d_subgrids, stream);
+  }
+  const auto *md = static_cast<const idg::Metadata *>(d_metadata);
+  HomeSort hs;
+  hipError_t err = home_sort(md, nr_subgrids, grid_size, S,
+                             std::max(0, nr_w_layers), stream, &hs);
+  if (err == hipSuccess) {
+    const int wps = S == 32 ? 1 : 2;  // workgroups per subgrid
+    hipLaunchKernelGGL(S == 32 ? kernel_splitter_fft<32>
+                               : kernel_splitter_fft<64>,
+                       dim3(nr_subgrids * wps), dim3(128), 0, stream,
+                       hs.order, static_cast<const float2 *>(d_grid),
+                       static_cast<float2 *>(d_subgrids), grid_size, -1.0f,
+                       scale);
     err = hipGetLastError();
   }
   return free_home_sort(hs, err, stream);

@@ -199,6 +199,11 @@ hipError_t launch_splitter(int nr_subgrids, int grid_size, int subgrid_size,
                            int nr_w_layers, const void *d_metadata,
                            const void *d_grid, void *d_subgrids,
                            hipStream_t stream);
+// launch_splitter then launch_subgrid_fft(-1, 1/S^2), fused for S = 32/64
+hipError_t launch_splitter_fft(int nr_subgrids, int grid_size,
+                               int subgrid_size, int nr_w_layers,
+                               const void *d_metadata, const void *d_grid,
+                               void *d_subgrids, hipStream_t stream);
 
 // Perf entry shared by p_run_gridder_/p_run_degridder_: env-configured
 // problem, synthetic inputs, timed launches.  Returns seconds per launch.

@@ -48,6 +48,7 @@ SIGNATURES = {
     "idg_subgrid_fft_launch": (_I, [_I, _I, _I, _F, _P, _P]),
     "idg_adder_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
     "idg_splitter_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "idg_splitter_fft_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
 }
 
 

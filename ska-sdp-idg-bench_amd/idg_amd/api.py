@@ -352,6 +352,21 @@ def splitter_launch(grid_size, metadata, grid, subgrids, nr_w_layers=1,
         "splitter_launch")
 
 
+def splitter_fft_launch(grid_size, metadata, grid, subgrids, nr_w_layers=1,
+                        stream=None):
+    """splitter_launch followed by subgrid_fft_launch(-1, 1/S^2): the
+    degridder's input subgrids from the grid (one fused kernel for S = 32 and
+    64, bit for bit the two launches' result)."""
+    import torch
+    ns, S = subgrids.shape[0], subgrids.shape[2]
+    _pipe_extents(ns, grid_size, S, nr_w_layers, metadata, subgrids, grid)
+    _check(lib.idg_splitter_fft_launch(
+        ns, grid_size, S, nr_w_layers, _dev_ptr(metadata, "metadata"),
+        _dev_ptr(grid, "grid", torch.float32),
+        _dev_ptr(subgrids, "subgrids", torch.float32), _stream_handle(stream)),
+        "splitter_fft_launch")
+
+
 def grid_onto(nr_subgrids, grid_size, subgrid_size, image_size,
               w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
               visibilities, spheroidal, aterms, metadata, grid,
@@ -375,15 +390,15 @@ def degrid_from(nr_subgrids, grid_size, subgrid_size, image_size,
                 w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
                 visibilities, spheroidal, aterms, metadata, grid,
                 nr_w_layers=1, subgrids=None, stream=None):
-    """uv grid -> visibilities: splitter, subgrid FFT (-1, 1/S^2), degridder
-    (overwrites the visibility rows of every subgrid)."""
+    """uv grid -> visibilities: splitter and subgrid FFT (-1, 1/S^2), fused
+    for S = 32 / 64 (splitter_fft_launch), then the degridder (overwrites
+    the visibility rows of every subgrid)."""
     import torch
     if subgrids is None:
         subgrids = torch.empty((nr_subgrids, 4, subgrid_size, subgrid_size, 2),
                                dtype=torch.float32, device=grid.device)
-    splitter_launch(grid_size, metadata, grid, subgrids, nr_w_layers, stream)
-    subgrid_fft_launch(subgrids, -1, 1.0 / (subgrid_size * subgrid_size),
-                       stream)
+    splitter_fft_launch(grid_size, metadata, grid, subgrids, nr_w_layers,
+                        stream)
     degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
                      w_step_in_lambda, nr_channels, nr_stations, uvw,
                      wavenumbers, visibilities, spheroidal, aterms, metadata,

@@ -104,6 +104,40 @@ def test_splitter_matches_numpy(idg, S, G, W):
     assert _rel(pl.to_complex(out.cpu().numpy()), ref) < 1e-6
 
 
+@pytest.mark.parametrize("S,G,W,ns", [(32, 128, 1, 40), (64, 160, 2, 40),
+                                      (24, 100, 2, 40), (32, 1024, 3, 3001),
+                                      (64, 512, 1, 777)])
+def test_splitter_fft_fused_matches_two_launches(idg, S, G, W, ns,
+                                                 monkeypatch):
+    """splitter_fft_launch = splitter_launch then subgrid_fft_launch(-1,
+    1/S^2), bit for bit: the fused kernel (S = 32, 64) against the two
+    launches (IDG_SPLIT_FFT=0), including subgrids off the grid edge and on
+    the skipped layer z = W (zeros), and against numpy.  S = 24 takes the two
+    launches either way."""
+    import torch
+    rng = np.random.default_rng(S * ns + W)
+    md, _ = _random_case(rng, G, S, W, ns)
+    t_md = _md_tensor(md)
+    g = torch.from_numpy(pl.to_pairs(
+        rng.normal(size=(W, 4, G, G)) + 1j * rng.normal(size=(W, 4, G, G)))
+    ).cuda()
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("IDG_SPLIT_FFT", fused)
+        out = torch.full((ns, 4, S, S, 2), 7.0, dtype=torch.float32,
+                         device="cuda")
+        idg.splitter_fft_launch(G, t_md, g, out, W)
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    # sign-bit equality too (zeros of skipped subgrids included)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    if ns <= 100:
+        ref = pl.subgrid_fft(pl.splitter(pl.to_complex(g.cpu().numpy()), md, S),
+                             -1, 1.0 / (S * S))
+        assert _rel(pl.to_complex(outs[0].cpu().numpy()), ref) < 2e-6
+
+
 @pytest.mark.parametrize("S,G,W", [(32, 128, 1), (16, 96, 3), (64, 160, 2),
                                    (24, 100, 2), (32, 512, 30)])
 def test_home_sort_forms_agree(idg, S, G, W, monkeypatch):
