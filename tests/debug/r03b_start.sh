@@ -17,4 +17,5 @@ print(d['value'], k['gridder']['ms'], k['degridder']['ms'], d['roofline']['frac'
 "
 timeout -k 10 400 python -u tests/debug/overlap.py > $out/overlap.txt 2>&1 || { tail -20 $out/overlap.txt; exit 1; }
 cat $out/overlap.txt
+bash tests/probes/profile_round.sh r03b
 echo all done

@@ -45,7 +45,8 @@ PIPELINE = ("kernel_subgrid_fft_reg", "kernel_subgrid_fft2", "kernel_subgrid_dft
             "kernel_home_count", "kernel_home_place", "kernel_home_scan",
             "kernel_home_key",
             "kernel_adder_bin_scan", "kernel_adder_bin", "kernel_adder",
-            "kernel_splitter_key", "kernel_splitter_pairs", "kernel_splitter")
+            "kernel_splitter_key", "kernel_splitter_pairs", "kernel_splitter",
+            "kernel_splitter_fft")
 
 
 def short_name(kernel_name):
