@@ -204,6 +204,20 @@ int idg_splitter_launch(int nr_subgrids, int grid_size, int subgrid_size,
                         const idg_cfloat_t *grid, idg_cfloat_t *subgrids,
                         void *stream);
 
+/* idg_gridder_launch followed by idg_subgrid_fft_launch(+1, 1.0f): the
+ * adder's input subgrids straight from the visibilities.  For S = 32 the FFT
+ * runs in the gridder's epilogue (the image-domain subgrids never reach
+ * HBM), bit for bit the two launches' result; other S <= 64 run the two
+ * launches.  Arguments as idg_gridder_launch. */
+int idg_gridder_fft_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                           float image_size, float w_step_in_lambda,
+                           int nr_channels, int nr_stations,
+                           const idg_uvw_t *uvw, const float *wavenumbers,
+                           const idg_cfloat_t *visibilities,
+                           const float *spheroidal, const idg_cfloat_t *aterms,
+                           const idg_metadata_t *metadata,
+                           idg_cfloat_t *subgrids, void *stream);
+
 /* idg_splitter_launch followed by idg_subgrid_fft_launch(-1, 1/S^2): the
  * degridder's input subgrids straight from the grid.  For S = 32 and 64 one
  * fused kernel (the uv-domain subgrids never reach HBM), bit for bit the

@@ -205,6 +205,25 @@ int idg_gridder_launch(int nr_subgrids, int grid_size, int subgrid_size,
                 metadata, subgrids, stream);
 }
 
+int idg_gridder_fft_launch(int nr_subgrids, int grid_size, int subgrid_size,
+                           float image_size, float w_step_in_lambda,
+                           int nr_channels, int nr_stations,
+                           const idg_uvw_t *uvw, const float *wavenumbers,
+                           const idg_cfloat_t *visibilities,
+                           const float *spheroidal, const idg_cfloat_t *aterms,
+                           const idg_metadata_t *metadata,
+                           idg_cfloat_t *subgrids, void *stream) {
+  if (subgrid_size > 64)
+    return fail(IDG_E_INVALID_ARGUMENT,
+                "idg_gridder_fft_launch: subgrid_size <= 64 (the FFT's)");
+  auto p = make_problem(nr_subgrids, grid_size, subgrid_size, image_size,
+                        w_step_in_lambda, nr_channels, nr_stations);
+  p.fft_out = true;
+  return launch(idg_mi355x::Direction::kGridder, p, uvw, wavenumbers,
+                const_cast<idg_cfloat_t *>(visibilities), spheroidal, aterms,
+                metadata, subgrids, stream);
+}
+
 int idg_degridder_launch(int nr_subgrids, int grid_size, int subgrid_size,
                          float image_size, float w_step_in_lambda,
                          int nr_channels, int nr_stations,

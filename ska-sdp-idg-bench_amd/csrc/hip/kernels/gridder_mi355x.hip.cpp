@@ -39,6 +39,7 @@
 
 #include "../util.hpp"
 #include "device.hpp"
+#include "fft.hpp"
 #include "lib-hip.hpp"
 #include "mfma.hpp"
 
@@ -164,11 +165,13 @@ __device__ __forceinline__ void timestep_mirror(
   }
 }
 
-// Epilogue for one pixel: P <- sph * A1^H P A2, correlation-planar store.
-__device__ __forceinline__ void store_pixel(
-    const float (&a)[8], int p, int S, int npix, const SubgridSetup &g,
-    int nr_stations, const float *__restrict__ spheroidal,
-    const float2 *__restrict__ aterms, float2 *__restrict__ out) {
+// Epilogue for one pixel: o = sph * A1^H P A2 (4 correlations) ...
+__device__ __forceinline__ void pixel_out(const float (&a)[8], int p, int S,
+                                          const SubgridSetup &g,
+                                          int nr_stations,
+                                          const float *__restrict__ spheroidal,
+                                          const float2 *__restrict__ aterms,
+                                          float2 (&o)[4]) {
   const int y = p / S, x = p - (p / S) * S;
   idg::cfloat pix[4], a1[4], a2[4];
   for (int q = 0; q < 4; ++q) pix[q] = {a[2 * q], a[2 * q + 1]};
@@ -179,9 +182,18 @@ __device__ __forceinline__ void store_pixel(
   idg::apply_aterm_gridder(pix, a1, a2);
   const float sph = spheroidal[p];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    out[static_cast<size_t>(q) * npix + p] =
-        make_float2(pix[q].re * sph, pix[q].im * sph);
+  for (int q = 0; q < 4; ++q) o[q] = make_float2(pix[q].re * sph, pix[q].im * sph);
+}
+
+// ... and its correlation-planar store.
+__device__ __forceinline__ void store_pixel(
+    const float (&a)[8], int p, int S, int npix, const SubgridSetup &g,
+    int nr_stations, const float *__restrict__ spheroidal,
+    const float2 *__restrict__ aterms, float2 *__restrict__ out) {
+  float2 o[4];
+  pixel_out(a, p, S, g, nr_stations, spheroidal, aterms, o);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[static_cast<size_t>(q) * npix + p] = o[q];
 }
 
 // W_TERMS = false: the caller guarantees w_offset = 0 (mirror subgrids), so
@@ -270,7 +282,11 @@ __device__ __forceinline__ void l2_prefetch_dma(const void *src,
       : "memory");
 }
 
-template <int S_CT, int PT, int CB, int NW, bool MIRROR>
+// FFT: the subgrid leaves as its 2-D FFT (sign +1, scale 1; S = 32 only),
+// what launch_subgrid_fft(+1, 1) would make of the plain output, bit for
+// bit: the pixels go to LDS planes instead of HBM and fft.hpp's transform
+// (kernel_subgrid_fft_reg's) runs on them (idg_gridder_fft_launch).
+template <int S_CT, int PT, int CB, int NW, bool MIRROR, bool FFT = false>
 __device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -659,9 +675,21 @@ __device__ __forceinline__ void grid_mfma(
         if constexpr (!kFused) obuf[(kPass + lp) * 16 + col] = accy[i][r];
       }
     __syncthreads();
-    for (int q = tid; q < kPass; q += NW * 64) {
+    // FFT: each thread's pixels stay in registers until every obuf row is
+    // read (the planes reuse that LDS)
+    static_assert(!FFT || (S_CT == 32 && kPass >= (MIRROR ? 512 : 1024)),
+                  "the FFT epilogue takes a whole S = 32 subgrid in one pass");
+    constexpr int kIt = FFT ? kPass / (NW * 64) : 1;
+    float2 keep[kIt][MIRROR ? 2 : 1][4];
+    auto emit = [&](const float (&a)[8], int p, int it, int slot) {
+      if constexpr (FFT)
+        pixel_out(a, p, S, g, nr_stations, spheroidal, aterms, keep[it][slot]);
+      else
+        store_pixel(a, p, S, npix, g, nr_stations, spheroidal, aterms, out);
+    };
+    auto body = [&](int q, int it) {
       const int b = gbase + q;
-      if (b >= half) continue;
+      if (b >= half) return;
       const float4 *xr = reinterpret_cast<const float4 *>(obuf + q * 16);
       const float4 xh0 = xr[0], xh1 = xr[1], xl0 = xr[2], xl1 = xr[3];
       const float x[8] = {xh0.x + xl0.x, xh0.y + xl0.y, xh0.z + xl0.z,
@@ -689,15 +717,49 @@ __device__ __forceinline__ void grid_mfma(
       for (int j = 0; j < 8; ++j)
         ab[j] = (kFused ? x[j] : x[j] + y[j]) * unscale;
       rotate4(ab, tc, ts);
-      store_pixel(ab, b, S, npix, g, nr_stations, spheroidal, aterms, out);
+      emit(ab, b, it, 0);
       if constexpr (MIRROR) {
         float am[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) am[j] = (x[j] - y[j]) * unscale;
         rotate4(am, tc, -ts);
-        store_pixel(am, npix - 1 - b, S, npix, g, nr_stations, spheroidal,
-                    aterms, out);
+        emit(am, npix - 1 - b, it, 1);
       }
+    };
+    if constexpr (FFT) {
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) body(tid + it * NW * 64, it);
+      constexpr int N = 32, RS = N + 1;
+      float2 *planes = reinterpret_cast<float2 *>(lds);  // [4][N][N + 1]
+      __syncthreads();  // every obuf row is read
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int b = tid + it * NW * 64;
+        if (b >= half) continue;
+#pragma unroll
+        for (int slot = 0; slot < (MIRROR ? 2 : 1); ++slot) {
+          const int p = slot ? npix - 1 - b : b;
+          const int row = p / N, col = p % N;
+#pragma unroll
+          for (int pol = 0; pol < 4; ++pol)
+            planes[pol * N * RS + row * RS + col] = keep[it][slot][pol];
+        }
+      }
+      __syncthreads();
+      float2 tw[N / 2];
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k) tw[k] = unit_phasor(k, N, 1.0f);
+      float2 f[N];
+      fft2_planes_lds<N>(planes, tid, 4 * N, tw, f);
+      if (tid < 4 * N) {
+        const int pp = tid / N, qq = tid % N;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+          out[static_cast<size_t>(pp) * npix + bit_reverse<N>(i) * N + qq] =
+              f[i];
+      }
+    } else {
+      for (int q = tid; q < kPass; q += NW * 64) body(q, 0);
     }
     __syncthreads();
   }
@@ -718,7 +780,7 @@ __device__ WgStamp idg_debug_timeline_gridder[kTimelineMax];
 // (One launch over every subgrid, each on its path: the reference's launch
 // shape.  The device entries launch the two-kernel form instead:
 // kernel_gridder_mirror_mi355x + kernel_gridder_general_mi355x.)
-template <int S_CT, int PPT, int CB, int MODE, int PT>
+template <int S_CT, int PPT, int CB, int MODE, int PT, bool FFT = false>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
                                   IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
@@ -758,14 +820,14 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
     timeline_start(idg_debug_timeline_gridder);
 #endif
     if (mirror)
-      grid_mfma<S_CT, PT, CB, NW, true>(g, S, npix, image_size, C,
-                                        nr_stations, uvw, wavenumbers,
-                                        visibilities, spheroidal, aterms, out,
-                                        lds);
+      grid_mfma<S_CT, PT, CB, NW, true, FFT>(g, S, npix, image_size, C,
+                                             nr_stations, uvw, wavenumbers,
+                                             visibilities, spheroidal, aterms,
+                                             out, lds);
     else
-      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
-          g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
-          visibilities, spheroidal, aterms, out, lds);
+      grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false,
+                FFT>(g, S, npix, image_size, C, nr_stations, uvw,
+                     wavenumbers, visibilities, spheroidal, aterms, out, lds);
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
     timeline_end(idg_debug_timeline_gridder);
 #endif
@@ -857,7 +919,7 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 //   workgroup returns at once.
 // queue: device.hpp queue_ints(nr_subgrids) ints of stream-ordered
 // workspace, its counters zeroed before the launches.
-template <int S_CT, int CB, int PT>
+template <int S_CT, int CB, int PT, bool FFT = false>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     kernel_gridder_mirror_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -886,13 +948,13 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
-  grid_mfma<S_CT, PT, CB, NW, true>(
+  grid_mfma<S_CT, PT, CB, NW, true, FFT>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds);
 }
 
-template <int S_CT, int CB, int PT>
+template <int S_CT, int CB, int PT, bool FFT = false>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     kernel_gridder_general_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -925,7 +987,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     const int s = all ? i : qv.at(i);
     const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
                                          image_size, w_step_in_lambda);
-    grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false>(
+    grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false, FFT>(
         g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
         visibilities, spheroidal, aterms,
         subgrids + static_cast<size_t>(s) * 4 * npix, lds);
@@ -945,6 +1007,16 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
 #define IDG_GRIDDER_GENERAL(S_)                                           \
   reinterpret_cast<const void *>(                                         \
       &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT>)
+// the FFT-epilogue instantiations (S = 32, MFMA only)
+#define IDG_GRIDDER_FFT32                                                 \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_mi355x<32, 4, 16, 1, IDG_GRID_PT, true>)
+#define IDG_GRIDDER_MIRROR_FFT32                                          \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_mirror_mi355x<32, 16, IDG_GRID_PT, true>)
+#define IDG_GRIDDER_GENERAL_FFT32                                         \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_gridder_general_mi355x<32, 16, IDG_GRID_PT, true>)
 
 // IDG_GRID_SPLIT=0: the device entries launch the one combined MFMA kernel
 // (A/B of the two-launch form).
@@ -964,12 +1036,24 @@ KernelChoice select_gridder(const Problem &p) {
   const bool mfma = gridder_impl() == 1;
   k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
   const void *part[2] = {nullptr, nullptr};
+  // the FFT in the gridder's epilogue (S = 32, MFMA; IDG_GRID_FFT=0: the
+  // launch layer runs launch_subgrid_fft after the plain gridder instead)
+  const char *fenv = std::getenv("IDG_GRID_FFT");
+  const bool fft_epilogue = p.fft_out && mfma && p.subgrid_size == 32 &&
+                            !(fenv != nullptr && fenv[0] == '0');
   switch (p.subgrid_size) {
     case 32:
       k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
       k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
       part[0] = IDG_GRIDDER_MIRROR(32, 4);
       part[1] = IDG_GRIDDER_GENERAL(32);
+      if (fft_epilogue) {
+        k.func = IDG_GRIDDER_FFT32;
+        k.name = "gridder_fft_mi355x_s32";
+        part[0] = IDG_GRIDDER_MIRROR_FFT32;
+        part[1] = IDG_GRIDDER_GENERAL_FFT32;
+        k.fft_in_kernel = true;
+      }
       break;
     case 64:
       k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);

@@ -29,23 +29,11 @@
 #include "../util.hpp"
 #include "common/types.hpp"
 #include "device.hpp"
+#include "fft.hpp"  // unit_phasor, cmulf, fft_dif_registers, bit_reverse
 
 namespace idg_mi355x {
 
 namespace {
-
-// exp(sign * 2 pi i * n / d) for integers, argument reduced exactly.
-__device__ __forceinline__ float2 unit_phasor(int n, int d, float sign) {
-  int r = n % d;
-  if (r < 0) r += d;
-  const float rev = static_cast<float>(r) / static_cast<float>(d);
-  return make_float2(__builtin_amdgcn_cosf(rev),
-                     sign * __builtin_amdgcn_sinf(rev));
-}
-
-__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
-  return make_float2(fma_(a.x, b.x, -(a.y * b.y)), fma_(a.x, b.y, a.y * b.x));
-}
 
 // Adder/splitter phasor of subgrid pixel (y, x): exp(i sgn pi ((x + y)(S + 1)
 // / S - 1)) = exp(2 pi i sgn ((x + y)(S + 1) - S) / (2 S)).
@@ -782,33 +770,6 @@ __global__ void __launch_bounds__(256)
 // takes 128 / N planes, loaded and stored coalesced.  Same transform as
 // kernel_subgrid_dft.
 template <int N>
-__device__ __forceinline__ void fft_dif_registers(float2 (&x)[N],
-                                                  const float2 (&tw)[N / 2]) {
-#pragma unroll
-  for (int len = N; len >= 2; len >>= 1) {
-    const int half = len >> 1;
-    const int step = N / len;  // twiddle stride
-#pragma unroll
-    for (int start = 0; start < N; start += len) {
-#pragma unroll
-      for (int j = 0; j < half; ++j) {
-        const float2 a = x[start + j], b = x[start + j + half];
-        x[start + j] = make_float2(a.x + b.x, a.y + b.y);
-        const float2 d = make_float2(a.x - b.x, a.y - b.y);
-        x[start + j + half] = j == 0 ? d : cmulf(d, tw[j * step]);
-      }
-    }
-  }
-}
-
-template <int N>
-__device__ __forceinline__ constexpr int bit_reverse(int i) {
-  int r = 0;
-  for (int b = 1; b < N; b <<= 1) r = (r << 1) | ((i & b) ? 1 : 0);
-  return r;
-}
-
-template <int N>
 __global__ void __launch_bounds__(128)
     kernel_subgrid_fft_reg(float2 *__restrict__ planes, int nr_planes,
                            float sign, float scale) {
@@ -871,82 +832,86 @@ __global__ void __launch_bounds__(128)
 }
 
 // The splitter and the degridding FFT (sign -1, scale 1/S^2) in one pass,
-// for S = 32 / 64: the uv-domain subgrid never goes to HBM.  A workgroup of
-// 128 threads takes P = 128 / N correlation planes of one subgrid (a whole
-// S = 32 subgrid, half an S = 64 one), in the home sort's order
-// (xcd_subgrid: consecutive workgroups of one XCD read overlapping grid
-// windows from its L2).  Every thread keeps one window column x (128 is a
-// multiple of N), so each wave-load reads whole grid-row segments; the
-// splitter's value cmulf(conj shift phasor, grid) goes straight to its
-// fftshifted place in the padded LDS planes, and the rest is
-// kernel_subgrid_fft_reg's transform: the same operations in the same order
-// as kernel_splitter_pairs followed by kernel_subgrid_fft_reg, so the output
-// is bit for bit theirs.  A subgrid not wholly inside the grid transforms
-// zeros, as the two-kernel path does.
+// for S = 32 / 64: the uv-domain subgrid never goes to HBM.  A unit of work
+// is P = 128 / N correlation planes of one subgrid (a whole S = 32 subgrid,
+// half an S = 64 one), taken in the home sort's order.  Persistent: a
+// resident grid (a multiple of 8 workgroups of 128 threads), the workgroups
+// of one XCD (blockIdx % 8) walking one contiguous eighth of the units, so
+// they read overlapping grid windows from that XCD's L2 (0.259 against
+// 0.271 ms for a workgroup per unit; loading the next unit's window behind
+// the current transform took 256 VGPRs and spilled, 0.271 ms).  Every
+// thread keeps one window column x (128 is a multiple of N), so each
+// wave-load reads whole grid-row segments; the splitter's value
+// cmulf(conj shift phasor, grid) goes straight to its fftshifted place in
+// the padded LDS planes, and the rest is kernel_subgrid_fft_reg's transform
+// (fft.hpp): the same operations in the same order as kernel_splitter_pairs
+// followed by kernel_subgrid_fft_reg, so the output is bit for bit theirs.
+// A subgrid not wholly inside the grid transforms zeros, as the two-kernel
+// path does (its window is read at the grid's origin, in bounds as G >= N,
+// and dropped).
 template <int N>
 __global__ void __launch_bounds__(128)
     kernel_splitter_fft(const int4 *__restrict__ order,
                         const float2 *__restrict__ grid,
-                        float2 *__restrict__ subgrids, int G, float sign,
-                        float scale) {
-  constexpr int P = 128 / N;   // planes per workgroup
-  constexpr int WPS = 4 / P;   // workgroups per subgrid
+                        float2 *__restrict__ subgrids, int G, int nunits,
+                        float sign, float scale) {
+  constexpr int P = 128 / N;   // planes per unit
+  constexpr int WPS = 4 / P;   // units per subgrid
   constexpr int RS = N + 1;    // padded LDS row stride (complex)
   constexpr int K = P * N * N / 128;  // window values per thread
   __shared__ float2 lds[P * N * RS];
   __shared__ float2 table[2 * N - 1];
   const int tid = threadIdx.x;
-  const int b = xcd_subgrid(blockIdx.x, gridDim.x);
-  // the home sort's entry {s, x, y, z}, z = -1 when not inside the grid
-  const int4 e = order[b / WPS];
-  const int pol0 = (b % WPS) * P;
-  const bool inside = e.w >= 0;
+  const int x = tid % N, y0 = tid / N, xs = half_shift(x, N);
+  const int J = gridDim.x / 8;             // workgroups per XCD
+  const int per = (nunits + 7) / 8;        // units per XCD
+  const int xcd = blockIdx.x % 8;
+  const int u1 = min(nunits, (xcd + 1) * per);
   for (int k = tid; k < 2 * N - 1; k += 128)
     table[k] = unit_phasor(k * (N + 1) - N, 2 * N, -1.0f);
-  const int x = tid % N, y0 = tid / N;
-  const float2 *gz =
-      grid + (static_cast<size_t>(inside ? e.w : 0) * 4 + pol0) * G * G +
-      static_cast<size_t>(inside ? e.z : 0) * G + (inside ? e.y : 0) + x;
-  // every grid load of the thread in flight before the first LDS write
-  float2 v[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int r = y0 + P * k;  // plane-major rows: plane r / N, row r % N
-    v[k] = inside ? gz[static_cast<size_t>(r / N) * G * G +
-                       static_cast<size_t>(r % N) * G]
-                  : make_float2(0.0f, 0.0f);
-  }
   float2 tw[N / 2];
 #pragma unroll
   for (int k = 0; k < N / 2; ++k) tw[k] = unit_phasor(k, N, sign);
+  // a wave-uniform base per row k plus the lane's 32-bit byte offset
+  const unsigned lane_off = static_cast<unsigned>((x + y0 * G) * 8);
   __syncthreads();  // table
-  const int xs = half_shift(x, N);
+  for (int u = xcd * per + blockIdx.x / 8; u < u1; u += J) {
+    // the home sort's entry {s, x, y, z}, z = -1 when not inside the grid
+    const int4 o = order[u / WPS];
+    const int4 e = make_int4(__builtin_amdgcn_readfirstlane(o.x),
+                             __builtin_amdgcn_readfirstlane(o.y),
+                             __builtin_amdgcn_readfirstlane(o.z),
+                             __builtin_amdgcn_readfirstlane(o.w));
+    const int pol0 = (u % WPS) * P;
+    const bool inside = e.w >= 0;
+    const char *gz = reinterpret_cast<const char *>(
+        grid + (static_cast<size_t>(inside ? e.w : 0) * 4 + pol0) * G * G +
+        static_cast<size_t>(inside ? e.z : 0) * G + (inside ? e.y : 0));
+    // rows r = y0 + P k: plane P k / N, row P k % N + y0 (y0 < P | N); every
+    // load of the thread in flight before the first LDS write
+    float2 v[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int r = y0 + P * k, pp = r / N, y = r % N;
-    lds[pp * N * RS + half_shift(y, N) * RS + xs] =
-        inside ? cmulf(table[x + y], v[k]) : v[k];
+    for (int k = 0; k < K; ++k)
+      v[k] = *reinterpret_cast<const float2 *>(
+          gz + (static_cast<size_t>(P * k / N) * G * G +
+                static_cast<size_t>(P * k % N) * G) * 8 + lane_off);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int r = y0 + P * k, pp = r / N, y = r % N;
+      lds[pp * N * RS + half_shift(y, N) * RS + xs] =
+          inside ? cmulf(table[x + y], v[k]) : make_float2(0.0f, 0.0f);
+    }
+    __syncthreads();
+    float2 f[N];
+    fft2_planes_lds<N>(lds, tid, 128, tw, f);
+    const int p = tid / N, q = tid % N;
+    float2 *out = subgrids + (static_cast<size_t>(e.x) * 4 + pol0 + p) * N * N;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      store_stream(&out[bit_reverse<N>(i) * N + q],
+                   make_float2(f[i].x * scale, f[i].y * scale));
+    __syncthreads();  // the planes are rewritten by the next unit
   }
-  __syncthreads();
-
-  const int p = tid / N, q = tid % N;  // plane, row (then column)
-  float2 f[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) f[i] = lds[p * N * RS + q * RS + i];
-  fft_dif_registers<N>(f, tw);
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    lds[p * N * RS + q * RS + bit_reverse<N>(i)] = f[i];
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < N; ++i) f[i] = lds[p * N * RS + i * RS + q];
-  fft_dif_registers<N>(f, tw);
-  float2 *out =
-      subgrids + (static_cast<size_t>(e.x) * 4 + pol0 + p) * N * N;
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    store_stream(&out[bit_reverse<N>(i) * N + q],
-                 make_float2(f[i].x * scale, f[i].y * scale));
 }
 
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
@@ -1124,14 +1089,23 @@ hipError_t launch_splitter_fft(int nr_subgrids, int grid_size,
   hipError_t err = home_sort(md, nr_subgrids, grid_size, S,
                              std::max(0, nr_w_layers), stream, &hs);
   if (err == hipSuccess) {
-    const int wps = S == 32 ? 1 : 2;  // workgroups per subgrid
-    hipLaunchKernelGGL(S == 32 ? kernel_splitter_fft<32>
-                               : kernel_splitter_fft<64>,
-                       dim3(nr_subgrids * wps), dim3(128), 0, stream,
-                       hs.order, static_cast<const float2 *>(d_grid),
-                       static_cast<float2 *>(d_subgrids), grid_size, -1.0f,
-                       scale);
-    err = hipGetLastError();
+    const int nunits = nr_subgrids * (S == 32 ? 1 : 2);
+    const void *func = S == 32
+                           ? reinterpret_cast<const void *>(
+                                 &kernel_splitter_fft<32>)
+                           : reinterpret_cast<const void *>(
+                                 &kernel_splitter_fft<64>);
+    // a multiple of 8 workgroups (whole XCD rows), at most the resident
+    // grid and at most one per unit (rounded up to the multiple of 8)
+    const int resident = std::max(8, resident_workgroups(func, 128) / 8 * 8);
+    const int nwg = std::min(resident, (nunits + 7) / 8 * 8);
+    int G = grid_size;
+    float sign = -1.0f, sc = scale;
+    const int4 *order = hs.order;
+    int nu = nunits;
+    void *args[] = {&order, const_cast<void **>(&d_grid), &d_subgrids, &G,
+                    &nu,    &sign,                         &sc};
+    err = hipLaunchKernel(func, dim3(nwg), dim3(128), args, 0, stream);
   }
   return free_home_sort(hs, err, stream);
 }

@@ -285,14 +285,19 @@ hipError_t launch(Direction dir, const Problem &p, const void *d_uvw,
                   &d_uvw,         &d_wavenumbers,   &d_visibilities,
                   &d_spheroidal,  &d_aterms,        &d_metadata,
                   &d_subgrids};
-  if (force || k.parts[1].func == nullptr)
-    return hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args,
-                           0, stream);
-  return launch_parts(k, p.nr_subgrids, args, p.w_step_in_lambda != 0.0f,
-                      stream);
+  const hipError_t err =
+      (force || k.parts[1].func == nullptr)
+          ? hipLaunchKernel(k.func, dim3(p.nr_subgrids), dim3(k.block), args,
+                            0, stream)
+          : launch_parts(k, p.nr_subgrids, args, p.w_step_in_lambda != 0.0f,
+                         stream);
+  if (err != hipSuccess || dir != Direction::kGridder || !p.fft_out ||
+      k.fft_in_kernel)
+    return err;
+  return launch_subgrid_fft(p.nr_subgrids, p.subgrid_size, +1, 1.0f,
+                            d_subgrids, stream);
 }
 
-namespace {
 // Workgroups of `func` (block threads) resident on the current device at
 // once: occupancy x CUs, cached per (device, kernel).
 int resident_workgroups(const void *func, int block) {
@@ -319,7 +324,6 @@ int resident_workgroups(const void *func, int block) {
   cache[key] = n;
   return n;
 }
-}  // namespace
 
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                         bool all_general, hipStream_t stream) {

@@ -97,6 +97,11 @@ struct Problem {
   float w_step_in_lambda = W_STEP;
   int nr_channels = 0;
   int nr_stations = 0;
+  // gridder only: the output subgrids are their 2-D FFT (sign +1, scale 1),
+  // as launch_subgrid_fft(+1, 1) after the plain gridder would make them
+  // (in the kernel's epilogue where KernelChoice::fft_in_kernel, else a
+  // launch_subgrid_fft after it)
+  bool fft_out = false;
 };
 
 // Buffer extents used for host-side validation (element counts).
@@ -113,6 +118,7 @@ struct KernelChoice {
   const char *name = "";
   int block = 256;
   int grid = 0;  // = nr_subgrids
+  bool fft_in_kernel = false;  // Problem::fft_out done by these kernels
   // The launch the device entries make instead, when parts[1] is set: one
   // kernel per subgrid class, each with the register allocation of its own
   // path.  parts[0] (kMirror; absent for odd S): grid =
@@ -186,6 +192,10 @@ int plan_host_chunks(const idg::Metadata *metadata, int nr_subgrids,
                      size_t moved, std::vector<int> *bounds,
                      std::vector<std::vector<std::pair<long long, long long>>>
                          *row_runs);
+
+// Workgroups of `func` (block threads) resident on the current device at
+// once: occupancy x CUs, cached per (device, kernel); 0 if the query fails.
+int resident_workgroups(const void *func, int block);
 
 // Pipeline steps (kernels/pipeline_mi355x.hip.cpp; include/idg_mi355x.h).
 hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,

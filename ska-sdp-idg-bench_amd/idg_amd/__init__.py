@@ -8,7 +8,8 @@ from .api import (IMAGE_SIZE, METADATA_DTYPE, NR_CORRELATIONS, W_STEP,
                   IdgError, abi_version, adder_launch, as_metadata,
                   bytes_gridder, c_run_degridder, c_run_gridder,
                   degrid_from, degridder_launch, device_name, flops_gridder,
-                  generate, grid_onto, gridder_launch, host_chunk_plan,
+                  generate, grid_onto, gridder_fft_launch, gridder_launch,
+                  host_chunk_plan,
                   kernel_name,
                   nr_subgrids_for, p_run_degridder, p_run_gridder,
                   splitter_fft_launch, splitter_launch, subgrid_fft_launch,
@@ -21,7 +22,7 @@ __all__ = [
     "abi_version", "adder_launch", "as_metadata", "bytes_gridder",
     "c_run_degridder", "c_run_gridder", "degrid_from", "degridder_launch",
     "device_name", "flops_gridder", "generate", "grid_onto",
-    "gridder_launch", "host_chunk_plan", "kernel_name", "nr_subgrids_for", "p_run_degridder",
+    "gridder_fft_launch", "gridder_launch", "host_chunk_plan", "kernel_name", "nr_subgrids_for", "p_run_degridder",
     "p_run_gridder", "splitter_fft_launch", "splitter_launch",
     "subgrid_fft_launch",
     "validate_metadata", "LIB_PATH", "shard",

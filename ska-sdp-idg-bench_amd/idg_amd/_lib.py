@@ -31,6 +31,8 @@ SIGNATURES = {
                                  _P, _P, _Z, _P, _P]),
     "idg_gridder_launch": (_I, [_I, _I, _I, _F, _F, _I, _I, _P, _P, _P, _P,
                                 _P, _P, _P, _P]),
+    "idg_gridder_fft_launch": (_I, [_I, _I, _I, _F, _F, _I, _I, _P, _P, _P,
+                                    _P, _P, _P, _P, _P]),
     "idg_degridder_launch": (_I, [_I, _I, _I, _F, _F, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _P, _P]),
     "idg_validate_metadata": (_I, [_I, _I, _I, _I, _Z, _Z, _P]),

@@ -274,6 +274,29 @@ def gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
         "gridder_launch")
 
 
+def gridder_fft_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                       w_step_in_lambda, nr_channels, nr_stations, uvw,
+                       wavenumbers, visibilities, spheroidal, aterms, metadata,
+                       subgrids, stream=None, validate=False):
+    """gridder_launch followed by subgrid_fft_launch(+1, 1.0): the adder's
+    input (uv-domain) subgrids; the FFT runs in the gridder's epilogue for
+    S = 32, bit for bit the two launches' result."""
+    import torch
+    f32 = torch.float32
+    _dev_extents(nr_subgrids, subgrid_size, nr_channels, nr_stations, uvw,
+                 wavenumbers, visibilities, spheroidal, aterms, metadata,
+                 subgrids, validate)
+    _check(lib.idg_gridder_fft_launch(
+        nr_subgrids, grid_size, subgrid_size, image_size, w_step_in_lambda,
+        nr_channels, nr_stations, _dev_ptr(uvw, "uvw", f32),
+        _dev_ptr(wavenumbers, "wavenumbers", f32),
+        _dev_ptr(visibilities, "visibilities", f32),
+        _dev_ptr(spheroidal, "spheroidal", f32),
+        _dev_ptr(aterms, "aterms", f32), _dev_ptr(metadata, "metadata"),
+        _dev_ptr(subgrids, "subgrids", f32), _stream_handle(stream)),
+        "gridder_fft_launch")
+
+
 def degridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
                      w_step_in_lambda, nr_channels, nr_stations, uvw,
                      wavenumbers, visibilities, spheroidal, aterms, metadata,
@@ -371,17 +394,17 @@ def grid_onto(nr_subgrids, grid_size, subgrid_size, image_size,
               w_step_in_lambda, nr_channels, nr_stations, uvw, wavenumbers,
               visibilities, spheroidal, aterms, metadata, grid,
               nr_w_layers=1, subgrids=None, stream=None):
-    """Visibilities -> uv grid: gridder, subgrid FFT (+1), adder into
-    `grid` (accumulates).  Returns the (uv-domain) subgrid scratch."""
+    """Visibilities -> uv grid: gridder and subgrid FFT (+1), fused for
+    S = 32 (gridder_fft_launch), then the adder into `grid` (accumulates).
+    Returns the (uv-domain) subgrid scratch."""
     import torch
     if subgrids is None:
         subgrids = torch.empty((nr_subgrids, 4, subgrid_size, subgrid_size, 2),
                                dtype=torch.float32, device=grid.device)
-    gridder_launch(nr_subgrids, grid_size, subgrid_size, image_size,
-                   w_step_in_lambda, nr_channels, nr_stations, uvw,
-                   wavenumbers, visibilities, spheroidal, aterms, metadata,
-                   subgrids, stream)
-    subgrid_fft_launch(subgrids, +1, 1.0, stream)
+    gridder_fft_launch(nr_subgrids, grid_size, subgrid_size, image_size,
+                       w_step_in_lambda, nr_channels, nr_stations, uvw,
+                       wavenumbers, visibilities, spheroidal, aterms,
+                       metadata, subgrids, stream)
     adder_launch(grid_size, metadata, subgrids, grid, nr_w_layers, stream)
     return subgrids
 

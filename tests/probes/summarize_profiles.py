@@ -56,6 +56,8 @@ def short_name(kernel_name):
     for tag, d, variant in KERNELS:
         if tag in kernel_name:
             args = kernel_name.split(tag, 1)[1].split(">", 1)[0].split(",")
+            if args[-1].strip() == "true":  # FFT epilogue: a pipeline kernel
+                return None
             if variant == "combined":
                 mode = int(args[3] if d == "gridder" else args[2])
                 if mode != 1:
@@ -65,6 +67,10 @@ def short_name(kernel_name):
 
 
 def pipeline_name(kernel_name):
+    for tag, d, variant in KERNELS:  # the gridder's FFT-epilogue kernels
+        if d == "gridder" and tag in kernel_name and \
+                kernel_name.split(tag, 1)[1].split(">", 1)[0].endswith("true"):
+            return "gridder_fft_" + variant
     for tag in PIPELINE:
         if "::" + tag + "<" in kernel_name or "::" + tag + "(" in kernel_name:
             return tag[len("kernel_"):]

@@ -895,3 +895,69 @@ def test_degridder_4_and_8_wave_workgroups_bitwise_on_ragged_batches(
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert (outs[0] != 7.25).any()
+
+
+@pytest.mark.parametrize("form", ["split", "combined"])
+@pytest.mark.parametrize("data", ["w0", "mixed", "wterm"])
+def test_gridder_fft_epilogue_matches_gridder_then_fft(idg, full, full_w,
+                                                       full_mixed, data, form,
+                                                       monkeypatch):
+    """gridder_fft_launch (S = 32: the subgrid FFT in the gridder's epilogue,
+    the adder's input without the image-domain subgrids in HBM) equals
+    gridder_launch followed by subgrid_fft_launch(+1, 1.0) bit for bit on
+    every subgrid of the full config: mirror subgrids, w-term subgrids (the
+    general path; 'wterm' takes the all-general launch), and a mixed batch
+    (the queue-fed general kernel), in the two-kernel form and the combined
+    kernel."""
+    import torch
+    p, a, dev = {"w0": full, "wterm": full_w, "mixed": full_mixed}[data]
+    monkeypatch.setenv("IDG_KERNEL_FORM", form)
+    ref = _dgrid(idg, p, dev, dev["visibilities"])
+    idg.subgrid_fft_launch(ref, +1, 1.0)
+    out = torch.full_like(ref, 7.25)
+    idg.gridder_fft_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                           dev["visibilities"], dev["spheroidal"],
+                           dev["aterms"], dev["metadata"], out)
+    torch.cuda.synchronize()
+    assert torch.equal(ref.view(torch.int32), out.view(torch.int32))
+
+
+@pytest.mark.parametrize("S", [32, 64])
+def test_gridder_fft_on_ragged_batches_and_fallback(idg, S, monkeypatch):
+    """Ragged and empty subgrids (nr_timesteps 0 .. T) with w != 0 on some:
+    gridder_fft_launch = the gridder then the FFT, bit for bit, for S = 32
+    (epilogue FFT) and S = 64 (two launches), and the same with the
+    epilogue turned off (IDG_GRID_FFT=0); and the transform is numpy's FFT
+    of the gridder's image-domain subgrids."""
+    import torch
+    st, ts, T, C, G = 6, 3, 40, 5, 512
+    a = idg.generate(st, ts, T, C, G, S)
+    md = a["metadata"].copy()
+    rng = np.random.default_rng(23 + S)
+    md["nr_timesteps"] = rng.integers(0, T + 1, md.size)
+    a["uvw"][1::4, :, 2] = rng.uniform(-100.0, 100.0,
+                                       a["uvw"][1::4, :, 2].shape)
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    dev = _to_device(dict(a, metadata=md))
+    ref = _dgrid(idg, p, dev, dev["visibilities"])
+    img = ref.clone()
+    idg.subgrid_fft_launch(ref, +1, 1.0)
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("IDG_GRID_FFT", env)
+        out = torch.full_like(ref, 7.25)
+        idg.gridder_fft_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                               dev["visibilities"], dev["spheroidal"],
+                               dev["aterms"], dev["metadata"], out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for out in outs:
+        assert torch.equal(ref.view(torch.int32), out.view(torch.int32))
+    # and the transform itself: numpy's FFT of the gridder's image-domain
+    # subgrids (sign +1, unnormalised)
+    import pipeline_oracle as pl
+    want = pl.subgrid_fft(pl.to_complex(img.cpu().numpy()), +1, 1.0)
+    got = pl.to_complex(outs[0].cpu().numpy())
+    assert np.abs(got - want).max() <= 2e-6 * max(np.abs(want).max(), 1e-30)
