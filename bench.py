@@ -628,26 +628,33 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
             e[6].record(stream)
     torch.cuda.synchronize()
     # the gridder with the FFT in its epilogue (S = 32; other S: the two
-    # launches), into a buffer of its own: gridder_ms + fft_ms's work
-    gev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    # launches) against the gridder followed by the FFT pass, the two
+    # interleaved rep by rep after one untimed rep of each (the same clock
+    # state for both), each into a buffer of its own
+    gev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)]
            for _ in range(npipe)]
     if has:
         nsub = sub_out.shape[0]
         p = (nsub, G, S, idg_amd.IMAGE_SIZE, w.get("w_step", idg_amd.W_STEP),
              w["nr_channels"], w["nr_stations"])
+        ins = (dev["uvw"], dev["wavenumbers"], dev["visibilities"],
+               dev["spheroidal"], dev["aterms"], dev["metadata"])
         for it in range(npipe + 1):
             e = gev[it - 1] if it > 0 else None
             if e:
                 e[0].record(stream)
-            idg_amd.gridder_fft_launch(*p, dev["uvw"], dev["wavenumbers"],
-                                       dev["visibilities"], dev["spheroidal"],
-                                       dev["aterms"], dev["metadata"],
-                                       uvfused, stream=stream)
+            idg_amd.gridder_launch(*p, *ins, uvsub, stream=stream)
+            idg_amd.subgrid_fft_launch(uvsub, +1, 1.0, stream=stream)
             if e:
                 e[1].record(stream)
+                e[2].record(stream)
+            idg_amd.gridder_fft_launch(*p, *ins, uvfused, stream=stream)
+            if e:
+                e[3].record(stream)
         torch.cuda.synchronize()
-    gridder_fft_ms = dist.max_over_ranks(
-        sum(e[0].elapsed_time(e[1]) for e in gev) / npipe if has else 0.0)
+    gridder_then_fft_ms, gridder_fft_ms = (
+        dist.max_over_ranks(sum(e[i].elapsed_time(e[i + 1]) for e in gev)
+                            / npipe if has else 0.0) for i in (0, 2))
 
     def avg(i, j):
         return dist.max_over_ranks(
@@ -663,9 +670,11 @@ def time_pipeline(w, dev, sub_out, stream, steps, world, dist):
                          "(idg_splitter_fft_launch), bit for bit "
                          "splitter_ms + ifft_ms's output"),
         "gridder_fft_ms": round(gridder_fft_ms, 4),
+        "gridder_then_fft_ms": round(gridder_then_fft_ms, 4),
         "gridder_fft": ("gridder with the FFT in its epilogue "
-                        "(idg_gridder_fft_launch), bit for bit the gridder "
-                        "(kernels.gridder.ms) + fft_ms's output"),
+                        "(idg_gridder_fft_launch) against the gridder "
+                        "followed by the FFT pass (bit for bit the same "
+                        "output), timed interleaved"),
         "grid": (f"[{nw}][4][{G}][{G}] complex64, "
                  f"{nw * G * G * 32 / 2**20:.0f} MiB"),
         "grid_reduce": (f"all_reduce(sum) of the ranks' partial grids, "
@@ -818,11 +827,13 @@ def main(argv=None):
                                           "ifft_ms")) / 1e3
         pipeline["full_cycle_mvis_s"] = round(
             nvis_job / (sec_per_step + extra) / 1e6, 2)
-        # the same cycle on the fused entries: gridder + FFT in one kernel,
-        # adder, grid sum, splitter + inverse FFT in one kernel, degridder
-        fused = (sec_per_step - t_grid + sum(
-            pipeline[k] for k in ("gridder_fft_ms", "adder_ms",
-                                  "grid_reduce_ms", "splitter_fft_ms")) / 1e3)
+        # the same cycle on the fused entries: the gridder with the FFT in
+        # its epilogue and the splitter + inverse FFT kernel, each priced
+        # by its difference to the launches it replaces, timed side by side
+        fused = (sec_per_step + extra + (
+            pipeline["gridder_fft_ms"] - pipeline["gridder_then_fft_ms"] +
+            pipeline["splitter_fft_ms"] - pipeline["splitter_ms"] -
+            pipeline["ifft_ms"]) / 1e3)
         pipeline["full_cycle_fused_mvis_s"] = round(nvis_job / fused / 1e6, 2)
         pipeline["note"] = ("gridder -> FFT -> adder -> grid-sum over ranks "
                             "and splitter -> FFT around the timed step; "
