@@ -1,6 +1,7 @@
 #!/bin/bash
-# The band adder (kernel_adder_band32): pipeline GPU tests on the band
-# build, then pipeline timings of the band build against the shipped one.
+# The band adder (kernel_adder_band32, measured 3.2x slower and removed;
+# DESIGN.md §11): pipeline GPU tests on the band build (ab/band.so, built
+# from that kernel), then pipeline timings of it against the shipped one.
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r03g
