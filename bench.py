@@ -474,6 +474,20 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled,
 # ---------------------------------------------------------------------------
 # Timed run
 # ---------------------------------------------------------------------------
+def dtype_label(kernels):
+    """The arithmetic of the kernels this run selected (idg_amd.kernel_name:
+    a `_valu` suffix is the all-VALU body, IDG_{GRIDDER,DEGRIDDER}_IMPL=valu,
+    whose MAC is plain f32 FMA; the others run the complex MAC on the f16
+    matrix core with two-term-split operands)."""
+    valu = {d: k["kernel"].endswith("_valu") for d, k in kernels.items()}
+    mfma = "f32 phase/accumulate, f16x2-split MFMA operands"
+    if all(valu.values()):
+        return "f32"
+    if not any(valu.values()):
+        return mfma
+    return "; ".join(f"{d}: {'f32' if v else mfma}" for d, v in valu.items())
+
+
 def upload(part):
     import numpy as np
     import torch
@@ -892,7 +906,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak" if args.mode == "replicated" else "strong",
         "vs_baseline": None,
-        "dtype": "f32 phase/accumulate, f16x2-split MFMA operands",
+        "dtype": dtype_label(kernels),
         "data": "synthetic (reference generators app/common/init.cpp, srand(0))",
         "config": {
             "workload": (f"{args.workload}: NR_STATIONS={w['nr_stations']} "

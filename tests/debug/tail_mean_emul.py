@@ -1,0 +1,92 @@
+"""Debug aid (CPU): the gridder's phase-reduction tail, emulated exactly and
+accumulated in double, scored in the reference metric (A-term and taper in
+double) against exact accumulation of the reference's f32 phases.
+
+  none      r = fma(ph, 1/2pi_hi, -m); only the phase_offset tail restored
+            after the sum (round 2)
+  block     + c = -k_b phase_index (1/2pi - 1/2pi_hi) added to every r of the
+            16-channel block (round 3: one v_pk_add per two phasors)
+  mean      no per-phasor add: the pixel's whole tail is restored after the
+            sum as one phasor exp(i tau (phase_offset - kbar pidx_bar)),
+            kbar the mean wavenumber, pidx_bar the phase index at the
+            subgrid's mean (u, v, w)
+
+    python tests/debug/tail_mean_emul.py [C] [T]
+DESIGN.md §3.3.
+"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests/debug"):
+    sys.path.insert(0, os.path.join(REPO, _p))
+import idg_amd  # noqa: E402
+import oracle as orc  # noqa: E402
+from mfma_accum_emul import IH, IH_LO, TAIL, f32, f64, fma32  # noqa: E402
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    T = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+    S, G = 32, 1024
+    a = idg_amd.generate(2, 2, T, C, G, S, nthreads=8)
+    ns = a["metadata"].size
+    img = f32(idg_amd.IMAGE_SIZE)
+    k = a["wavenumbers"].astype(f32)
+    npix = S * S
+    idx = ((np.arange(S) + 0.5 - S / 2) * f64(img) / S).astype(f32)
+    l = np.broadcast_to(idx[None, :], (S, S)).astype(f32).ravel()
+    m = np.broadcast_to(idx[:, None], (S, S)).astype(f32).ravel()
+    at = a["aterms"].reshape(-1, 2, S, S, 4, 2)
+    at = at[..., 0].astype(f64) + 1j * at[..., 1]
+    sph = a["spheroidal"].reshape(npix).astype(f64)
+    models = ("none", "block", "mean")
+    outs = {x: np.zeros((ns, 4, S, S, 2), f32) for x in models + ("exact",)}
+    for s in range(ns):
+        md = a["metadata"][s]
+        su = 2 * np.pi / f64(img)
+        uo = f32((int(md["x"]) + S // 2 - G // 2) * su)
+        vo = f32((int(md["y"]) + S // 2 - G // 2) * su)
+        poff = fma32(uo, l, (vo * m).astype(f32))
+        rows = slice(int(md["time_offset"]), int(md["time_offset"]) + T)
+        uvw = a["uvw"].reshape(-1, 3)[rows]
+        vis = a["visibilities"].reshape(-1, C, 4, 2)[rows]
+        V = vis[..., 0].astype(f64) + 1j * vis[..., 1]
+        P = {x: np.zeros((npix, 4), complex) for x in models + ("exact",)}
+        kb = k[(np.arange(C) // 16) * 16]
+        for t in range(T):
+            pidx = fma32(uvw[t, 0], l, (uvw[t, 1] * m).astype(f32))
+            ph = fma32(-pidx[None, :], k[:, None], poff[None, :])  # [C][npix]
+            P["exact"] += np.exp(1j * ph.astype(f64)).T @ V[t]
+            A = fma32(-pidx[None, :], kb[:, None], poff[None, :])
+            nm = -np.rint((A * IH).astype(f32))
+            r0 = fma32(ph, IH, nm)
+            cr = (-pidx[None, :] * (kb * IH_LO).astype(f32)[:, None]).astype(f32)
+            rb = (r0 + cr).astype(f32)
+            for x, r in (("none", r0), ("block", rb), ("mean", r0)):
+                P[x] += np.exp(2j * np.pi * r.astype(f64)).T @ V[t]
+        tail = np.exp(1j * poff.astype(f64) * f64(TAIL))
+        ubar, vbar = uvw[:, 0].astype(f64).mean(), uvw[:, 1].astype(f64).mean()
+        pbar = ubar * l.astype(f64) + vbar * m.astype(f64)
+        kbar = k.astype(f64).mean()
+        rot = {"none": tail, "block": tail,
+               "mean": np.exp(1j * f64(TAIL) * (poff.astype(f64) - kbar * pbar))}
+        a1 = at[int(md["aterm_index"]), int(md["station1"])].reshape(npix, 2, 2)
+        a2 = at[int(md["aterm_index"]), int(md["station2"])].reshape(npix, 2, 2)
+        for x in P:
+            Px = P[x] * (rot[x][:, None] if x in rot else 1.0)
+            Q = np.conj(np.transpose(a1, (0, 2, 1))) @ Px.reshape(npix, 2, 2) @ a2
+            Q = Q.reshape(npix, 4) * sph[:, None]
+            outs[x][s, ..., 0] = Q.real.T.reshape(4, S, S)
+            outs[x][s, ..., 1] = Q.imag.T.reshape(4, S, S)
+    o = orc.Oracle()
+    print(f"C={C} T={T}, {ns} subgrids: emulated reduction vs exact "
+          "(double sums), reference metric")
+    for x in models:
+        print(f"  {x:6s} {o.check_error(outs[x], outs['exact'])[0]:.3e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -256,6 +256,17 @@ def _warmup_worker(rank, world, port, out_dir):
     dist.finalize()
 
 
+def test_dtype_label_follows_the_selected_kernels():
+    import bench
+    mf = {"kernel": "gridder_mi355x_s32"}
+    va = {"kernel": "gridder_mi355x_s32_valu"}
+    assert bench.dtype_label({"gridder": mf, "degridder": mf}).startswith(
+        "f32 phase/accumulate, f16x2-split")
+    assert bench.dtype_label({"gridder": va, "degridder": va}) == "f32"
+    mixed = bench.dtype_label({"gridder": va, "degridder": mf})
+    assert mixed.startswith("gridder: f32; degridder: f32 phase")
+
+
 def test_extra_warmup_steps():
     import bench
     assert bench.extra_warmup_steps(0.015, 1.0) == 67   # configs[1], N = 1
