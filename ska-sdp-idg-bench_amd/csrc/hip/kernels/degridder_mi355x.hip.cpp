@@ -153,12 +153,26 @@ struct DegridMfmaLds {
 // tail_k_rev).  A dependent packed-f32 VALU pair gets one wait state
 // (s_nop 0), as hipcc pads its own; the output is read by compiler code,
 // which pads after the asm itself.
-template <int H>
+// TAIL = false: the same without c (two v_pk_fma_f32).
+template <int H, bool TAIL = true>
 __device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
                                                    floatx2 o, floatx2 nm,
                                                    floatx2 cr) {
   floatx2 r;
-  if constexpr (H == 0)
+  if constexpr (!TAIL && H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel_hi:[1,0,0]"
+        : "=&v"(r)
+        : "v"(p), "s"(kp), "v"(o), "v"(nm));
+  else if constexpr (!TAIL)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,1,1]\n\t"
+        "s_nop 0\n\t"
+        "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel:[0,0,1] "
+        "op_sel_hi:[1,0,1]"
+        : "=&v"(r)
+        : "v"(p), "s"(kp), "v"(o), "v"(nm));
+  else if constexpr (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]\n\t"
         "s_nop 0\n\t"
         "v_pk_fma_f32 %0, %0, 0.15915494, %4 op_sel_hi:[1,0,0]\n\t"
@@ -179,7 +193,8 @@ __device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
 }
 static_assert(kInv2PiHi == 0.15915494f, "phase_rev_bcast's inline constant");
 
-template <int S_CT, int CT, int CB, int KP, bool MIRROR, int NW>
+template <int S_CT, int CT, int CB, int KP, bool MIRROR, int NW,
+          bool TAIL = true>
 __device__ __forceinline__ void degrid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -394,7 +409,8 @@ __device__ __forceinline__ void degrid_mfma(
             const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
             // the k * phase_index part of the reduction's tail at the
             // block's first channel (phase = k * phase_index - poff here)
-            const floatx2 cr = tail_k_rev(pidx, kk[jb]);
+            floatx2 cr = {0.0f, 0.0f};
+            if constexpr (TAIL) cr = tail_k_rev(pidx, kk[jb]);
             // Packed over channel pairs (j, j+1) per pixel: the wavenumber
             // pair is one SGPR pair and the pixel's terms are broadcast from
             // their halves of the (pixel 0, pixel 1) pairs by op_sel, so the
@@ -403,8 +419,10 @@ __device__ __forceinline__ void degrid_mfma(
 #pragma unroll
             for (int j = jb; j < jb + CB; j += 2) {
               const floatx2 kp = {kk[j], kk[j + 1]};
-              const floatx2 rx = phase_rev_bcast<0>(pidx, kp, npoff, nm, cr);
-              const floatx2 ry = phase_rev_bcast<1>(pidx, kp, npoff, nm, cr);
+              const floatx2 rx =
+                  phase_rev_bcast<0, TAIL>(pidx, kp, npoff, nm, cr);
+              const floatx2 ry =
+                  phase_rev_bcast<1, TAIL>(pidx, kp, npoff, nm, cr);
               float s0, c0, s1, c1, s2, c2, s3, c3;
               sincos_rev(rx.x, &s0, &c0);  // channel j,   pixel 0
               sincos_rev(ry.x, &s1, &c1);  // channel j,   pixel 1
@@ -438,12 +456,8 @@ __device__ __forceinline__ void degrid_mfma(
 #pragma unroll
           for (int j = 0; j < CT; j += 2) {
             const float v0 = acc[j][r], v1 = acc[j + 1][r];
-            const float s0 = v0 + __builtin_bit_cast(float,
-                __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v0),
-                                            0x128, 0xF, 0xF, false));
-            const float s1 = v1 + __builtin_bit_cast(float,
-                __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v1),
-                                            0x128, 0xF, 0xF, false));
+            const float s0 = v0 + row_ror8(v0);
+            const float s1 = v1 + row_ror8(v1);
             const float out = (col < 8 ? s0 : s1) * unscale;
             if (pc0 == 0)
               dst[8 * j] = out;
@@ -489,7 +503,7 @@ __device__ WgStamp idg_debug_timeline_degridder[kTimelineMax];
 // (One launch over every subgrid, each on its path: the reference's launch
 // shape.  The device entries launch the two-kernel form instead:
 // kernel_degridder_mirror_mi355x + kernel_degridder_general_mi355x.)
-template <int S_CT, int CG, int MODE, int CT, int NW>
+template <int S_CT, int CG, int MODE, int CT, int NW, bool TAIL = true>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
                                   MODE == 1 ? IDG_DEGRID_WAVES : 1)
     kernel_degridder_mi355x(const int grid_size, int subgrid_size,
@@ -532,11 +546,11 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
     timeline_start(idg_debug_timeline_degridder);
 #endif
     if (eligible)
-      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW, TAIL>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
           visibilities, spheroidal, aterms, sg, lds);
     else
-      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+      degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW, TAIL>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
           visibilities, spheroidal, aterms, sg, lds);
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
@@ -668,7 +682,7 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
 // K-block of the 512), so an S = 32 subgrid is one chunk and its
 // visibilities are written once (the combined kernel's 512-pixel chunks
 // read them back and wrote them again).
-template <int S_CT, int CT, int NW>
+template <int S_CT, int CT, int NW, bool TAIL = true>
 __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
     kernel_degridder_mirror_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -702,13 +716,13 @@ __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
     if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
-  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW>(
+  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW, TAIL>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds);
 }
 
-template <int S_CT, int CT>
+template <int S_CT, int CT, bool TAIL = true>
 __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     kernel_degridder_general_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -741,7 +755,7 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     const int s = all ? i : qv.at(i);
     const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
                                          image_size, w_step_in_lambda);
-    degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+    degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW, TAIL>(
         g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
         visibilities, spheroidal, aterms,
         subgrids + static_cast<size_t>(s) * 4 * npix, lds);
@@ -760,7 +774,7 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
 // computation, valid for any subgrid.  On a w-term batch this runs 2-3 %
 // faster than the queue-fed general kernel above, whose workgroups loop
 // over subgrids.
-template <int S_CT, int CT>
+template <int S_CT, int CT, bool TAIL = true>
 __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     kernel_degridder_general_direct_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -779,21 +793,40 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
   const int s = xcd_subgrid(blockIdx.x, gridDim.x);
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);
-  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW>(
+  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, false, NW, TAIL>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds);
 }
 
-#define IDG_DEGRIDDER(S_, CG_, MODE_, NW_) \
-  reinterpret_cast<const void *>(                   \
-      &kernel_degridder_mi355x<S_, CG_, MODE_, IDG_DEGRID_CT, NW_>)
-#define IDG_DEGRIDDER_MIRROR(S_, NW_)                   \
-  reinterpret_cast<const void *>(                      \
-      &kernel_degridder_mirror_mi355x<S_, IDG_DEGRID_CT, NW_>)
-#define IDG_DEGRIDDER_GENERAL(S_)                      \
-  reinterpret_cast<const void *>(                      \
-      &kernel_degridder_general_mi355x<S_, IDG_DEGRID_CT>)
+#define IDG_DEGRIDDER_VALU(S_, CG_)                                       \
+  reinterpret_cast<const void *>(                                         \
+      &kernel_degridder_mi355x<S_, CG_, 0, IDG_DEGRID_CT, 4>)
+
+// The MFMA kernels of one (S, waves per workgroup, tail): the combined
+// kernel and the two-kernel form's mirror, queue-fed general and direct
+// all-general kernels.
+struct DegridderSet {
+  const void *combined, *mirror, *general, *general_direct;
+};
+template <int S_, int NW_, bool TAIL_>
+DegridderSet degridder_set() {
+  return {reinterpret_cast<const void *>(
+              &kernel_degridder_mi355x<S_, 4, 1, IDG_DEGRID_CT, NW_, TAIL_>),
+          reinterpret_cast<const void *>(
+              &kernel_degridder_mirror_mi355x<S_, IDG_DEGRID_CT, NW_, TAIL_>),
+          reinterpret_cast<const void *>(
+              &kernel_degridder_general_mi355x<S_, IDG_DEGRID_CT, TAIL_>),
+          reinterpret_cast<const void *>(
+              &kernel_degridder_general_direct_mi355x<S_, IDG_DEGRID_CT,
+                                                      TAIL_>)};
+}
+template <int S_>
+DegridderSet degridder_set_for(bool nw8, bool tail) {
+  if (nw8)
+    return tail ? degridder_set<S_, 8, true>() : degridder_set<S_, 8, false>();
+  return tail ? degridder_set<S_, 4, true>() : degridder_set<S_, 4, false>();
+}
 
 // IDG_DEGRID_SPLIT=0: the device entries launch the one combined MFMA
 // kernel (A/B of the two-launch form).
@@ -824,41 +857,28 @@ KernelChoice select_degridder(const Problem &p) {
   // IDG_DEGRID_NW=4 / 8 forces the workgroup size (tests; read per call)
   if (const char *v = std::getenv("IDG_DEGRID_NW"))
     nw8 = mfma && std::string(v) == "8";
-#define IDG_PICK(CG_, MODE_, NW_)                                          \
-  (s32 ? IDG_DEGRIDDER(32, CG_, MODE_, NW_)                                \
-       : (s64 ? IDG_DEGRIDDER(64, CG_, MODE_, NW_)                         \
-              : IDG_DEGRIDDER(0, CG_, MODE_, NW_)))
   if (mfma) {
+    k.prec = precision_for(Direction::kDegridder, p);
+    const bool tail = (k.prec & kPrecTail) != 0;
+    const DegridderSet set = s32   ? degridder_set_for<32>(nw8, tail)
+                             : s64 ? degridder_set_for<64>(nw8, tail)
+                                   : degridder_set_for<0>(nw8, tail);
     // the MFMA kernel has no CG
-    k.func = nw8 ? IDG_PICK(4, 1, 8) : IDG_PICK(4, 1, 4);
+    k.func = set.combined;
     k.block = nw8 ? 512 : 256;
     if (IDG_DEGRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
       // mirror-eligible subgrids (even S only), then the others on 8-wave
       // workgroups with 1,024-pixel chunks
-#define IDG_PICK_MIRROR(NW_)                                               \
-  (s32 ? IDG_DEGRIDDER_MIRROR(32, NW_)                                     \
-       : (s64 ? IDG_DEGRIDDER_MIRROR(64, NW_) : IDG_DEGRIDDER_MIRROR(0, NW_)))
       if (p.subgrid_size % 2 == 0)
-        k.parts[0] = {nw8 ? IDG_PICK_MIRROR(8) : IDG_PICK_MIRROR(4), k.block,
-                      KernelChoice::kMirror};
-      k.parts[1] = {s32 ? IDG_DEGRIDDER_GENERAL(32)
-                        : (s64 ? IDG_DEGRIDDER_GENERAL(64)
-                               : IDG_DEGRIDDER_GENERAL(0)),
-                    512, KernelChoice::kGeneral};
-      k.all_general = {
-          reinterpret_cast<const void *>(
-              s32 ? &kernel_degridder_general_direct_mi355x<32, IDG_DEGRID_CT>
-                  : (s64 ? &kernel_degridder_general_direct_mi355x<
-                               64, IDG_DEGRID_CT>
-                         : &kernel_degridder_general_direct_mi355x<
-                               0, IDG_DEGRID_CT>)),
-          512, KernelChoice::kPlain};
-#undef IDG_PICK_MIRROR
+        k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror};
+      k.parts[1] = {set.general, 512, KernelChoice::kGeneral};
+      k.all_general = {set.general_direct, 512, KernelChoice::kPlain};
     }
   } else {
-    k.func = cg8 ? IDG_PICK(8, 0, 4) : IDG_PICK(4, 0, 4);
+    k.func = s32   ? (cg8 ? IDG_DEGRIDDER_VALU(32, 8) : IDG_DEGRIDDER_VALU(32, 4))
+             : s64 ? (cg8 ? IDG_DEGRIDDER_VALU(64, 8) : IDG_DEGRIDDER_VALU(64, 4))
+                   : (cg8 ? IDG_DEGRIDDER_VALU(0, 8) : IDG_DEGRIDDER_VALU(0, 4));
   }
-#undef IDG_PICK
   if (mfma)
     k.name = s32 ? "degridder_mi355x_s32"
                  : (s64 ? "degridder_mi355x_s64" : "degridder_mi355x_generic");

@@ -65,6 +65,13 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
   return neg_pidx * floatx2{f, f};
 }
 
+// Precision options of the MFMA kernels (template PREC, chosen per launch by
+// util.cpp precision_for): kPrecTail adds tail_k_rev to every phasor's
+// revolutions; kPrecFlush (gridder, S = 32) sums the accumulator tiles into
+// an f32 master every kFlushFills fills (at most 32 K-steps each).
+constexpr int kPrecTail = 1, kPrecFlush = 2;
+constexpr int kFlushFills = 4;
+
 // exp(i * phase_offset * kPhaseTail), |angle| <= 1.4e-4: cos = 1 - a^2/2
 // (the a^4 term is below 1e-16), sin = a (the a^3 term below 5e-13).
 __device__ __forceinline__ void phase_tail(float phase_offset, float *c,
@@ -72,6 +79,16 @@ __device__ __forceinline__ void phase_tail(float phase_offset, float *c,
   const float a = phase_offset * kPhaseTail;
   *c = fma_(-0.5f * a, a, 1.0f);
   *s = a;
+}
+
+// The value of lane (l + 8) mod 16 of the lane's 16-lane row (DPP
+// row_ror:8).  Call it on a named scalar: applied to the elements of an
+// ext_vector in a loop, this hipcc emitted one DPP move of element 0 for
+// all of them (tests/probes/dpp_vector_probe.hip).
+__device__ __forceinline__ float row_ror8(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128,
+                                         0xF, 0xF, false));
 }
 
 // The 4 correlations (re, im interleaved) times the phasor (c, s).

@@ -286,7 +286,17 @@ __device__ __forceinline__ void l2_prefetch_dma(const void *src,
 // what launch_subgrid_fft(+1, 1) would make of the plain output, bit for
 // bit: the pixels go to LDS planes instead of HBM and fft.hpp's transform
 // (kernel_subgrid_fft_reg's) runs on them (idg_gridder_fft_launch).
-template <int S_CT, int PT, int CB, int NW, bool MIRROR, bool FFT = false>
+// PREC: kPrecTail adds the k * phase_index part of the reduction's tail to
+// every phasor's revolutions (device.hpp tail_k_rev: one v_pk_add_f32 per
+// two phasors, ~5 % of the MFMA loop); kPrecFlush (S = 32) adds the
+// accumulator tiles to an f32 master every kFlushFills fills and restarts
+// them from zero (blocked summation, DESIGN.md §3.1: the MFMA rounds its
+// f32 sum several times per instruction, so 2,048 K-steps into one tile put
+// the C = 256 gridder 8.4e-6 from exact accumulation).  The master lives in
+// the subgrid's own output slot (32 KB at S = 32, one pass), which only the
+// epilogue writes, after the master is read back.
+template <int S_CT, int PT, int CB, int NW, bool MIRROR, bool FFT = false,
+          int PREC = kPrecTail>
 __device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -383,6 +393,36 @@ __device__ __forceinline__ void grid_mfma(
     for (int i = 0; i < PT; ++i) accx[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < PY; ++i) accy[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // Blocked summation (PREC & kPrecFlush): lane (grp, col < 8) of tile t
+    // owns master word block ((wave * AT + t) * 32 + grp * 8 + col) of the
+    // subgrid's output slot, 4 floats (its 4 rows); the hi and lo columns
+    // of a component (lanes col and col + 8) are summed into it by one DPP
+    // row_ror:8 add.  The master is kept unscaled (x 2^e, exact).
+    constexpr bool kFlush = (PREC & kPrecFlush) != 0;
+    static_assert(!kFlush || S_CT == 32,
+                  "the master fills the S = 32 output slot in one pass");
+    bool flushed = false;
+    auto master = [&](int t) {
+      return reinterpret_cast<float4 *>(out) +
+             ((wave * AT + t) * 32 + grp * 8 + (col & 7));
+    };
+    // (the four elements are taken into named scalars before their DPP
+    // moves: written as a loop over a[r], this hipcc moved a[0] four times;
+    // tests/probes/dpp_vector_probe.hip)
+    auto flush_tile = [&](floatx4 &a, int t, float unsc) {
+      const float a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+      const float v0 = (a0 + row_ror8(a0)) * unsc;
+      const float v1 = (a1 + row_ror8(a1)) * unsc;
+      const float v2 = (a2 + row_ror8(a2)) * unsc;
+      const float v3 = (a3 + row_ror8(a3)) * unsc;
+      if (col < 8) {
+        float4 m = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (flushed) m = *master(t);
+        *master(t) = make_float4(m.x + v0, m.y + v1, m.z + v2, m.w + v3);
+      }
+      a = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    };
 
     for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
       const int nq = min(quads_per_fill, nquads - q0);
@@ -558,7 +598,8 @@ __device__ __forceinline__ void grid_mfma(
                 const floatx2 nm = {-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
                 // the k * phase_index part of the reduction's tail, at the
                 // block's first channel (device.hpp: kPhaseTail)
-                const floatx2 cr = tail_k_rev(np, ka);
+                floatx2 cr = {0.0f, 0.0f};
+                if constexpr ((PREC & kPrecTail) != 0) cr = tail_k_rev(np, ka);
 #pragma unroll
                 for (int u = 0; u < CB / 4; ++u) {
                   const int jj = jb + u;
@@ -574,8 +615,8 @@ __device__ __forceinline__ void grid_mfma(
                     const float kj = kb[4 * u + j];
                     const floatx2 ph =
                         __builtin_elementwise_fma(np, floatx2{kj, kj}, PG2[h]);
-                    const floatx2 r =
-                        __builtin_elementwise_fma(ph, ih, nm) + cr;
+                    floatx2 r = __builtin_elementwise_fma(ph, ih, nm);
+                    if constexpr ((PREC & kPrecTail) != 0) r = r + cr;
                     sincos_rev(r.x, &snx[j], &csx[j]);
                     sincos_rev(r.y, &sny[j], &csy[j]);
                   }
@@ -611,7 +652,8 @@ __device__ __forceinline__ void grid_mfma(
               NM[h] = floatx2{-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
               // the k * phase_index part of the reduction's tail at the
               // block's first channel (device.hpp: kPhaseTail)
-              CR[h] = tail_k_rev(NP[h], ka);
+              if constexpr ((PREC & kPrecTail) != 0)
+                CR[h] = tail_k_rev(NP[h], ka);
             }
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
@@ -633,8 +675,8 @@ __device__ __forceinline__ void grid_mfma(
                   const float kj = kb[4 * u + j];
                   const floatx2 ph =
                       __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
-                  const floatx2 r =
-                      __builtin_elementwise_fma(ph, ih, NM[h]) + CR[h];
+                  floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
+                  if constexpr ((PREC & kPrecTail) != 0) r = r + CR[h];
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
@@ -657,6 +699,40 @@ __device__ __forceinline__ void grid_mfma(
               // wave per SIMD; DESIGN.md §4.4, tests/debug/diff_detail.py).
               IDG_KSTEP_FENCE();
             }
+          }
+        }
+        if constexpr (kFlush) {
+          // every kFlushFills fills except the last (wave-uniform)
+          const bool last =
+              j0 + cq_per_fill >= nchq && q0 + quads_per_fill >= nquads;
+          if (!last && (fidx + 1) % kFlushFills == 0) {
+            const float unsc = ldexpf(1.0f, e);
+#pragma unroll
+            for (int i = 0; i < PT; ++i) flush_tile(accx[i], i, unsc);
+            if constexpr (!kFused) {
+#pragma unroll
+              for (int i = 0; i < PY; ++i) flush_tile(accy[i], PT + i, unsc);
+            }
+            flushed = true;
+          }
+        }
+      }
+    }
+    if constexpr (kFlush) {
+      // the master back into the hi columns (lanes col < 8), rescaled to
+      // the current 2^-e (exact); the epilogue sums hi + lo as before
+      if (flushed && col < 8) {
+        const float sc = ldexpf(1.0f, -e);
+#pragma unroll
+        for (int i = 0; i < PT; ++i) {
+          const float4 m = *master(i);
+          accx[i] += floatx4{m.x, m.y, m.z, m.w} * sc;
+        }
+        if constexpr (!kFused) {
+#pragma unroll
+          for (int i = 0; i < PY; ++i) {
+            const float4 m = *master(PT + i);
+            accy[i] += floatx4{m.x, m.y, m.z, m.w} * sc;
           }
         }
       }
@@ -780,7 +856,8 @@ __device__ WgStamp idg_debug_timeline_gridder[kTimelineMax];
 // (One launch over every subgrid, each on its path: the reference's launch
 // shape.  The device entries launch the two-kernel form instead:
 // kernel_gridder_mirror_mi355x + kernel_gridder_general_mi355x.)
-template <int S_CT, int PPT, int CB, int MODE, int PT, bool FFT = false>
+template <int S_CT, int PPT, int CB, int MODE, int PT, bool FFT = false,
+          int PREC = kPrecTail>
 __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
                                   IDG_GRID_WAVES)
     kernel_gridder_mi355x(const int grid_size, int subgrid_size,
@@ -820,14 +897,14 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
     timeline_start(idg_debug_timeline_gridder);
 #endif
     if (mirror)
-      grid_mfma<S_CT, PT, CB, NW, true, FFT>(g, S, npix, image_size, C,
-                                             nr_stations, uvw, wavenumbers,
-                                             visibilities, spheroidal, aterms,
-                                             out, lds);
+      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC>(
+          g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms, out, lds);
     else
       grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false,
-                FFT>(g, S, npix, image_size, C, nr_stations, uvw,
-                     wavenumbers, visibilities, spheroidal, aterms, out, lds);
+                FFT, PREC>(g, S, npix, image_size, C, nr_stations, uvw,
+                           wavenumbers, visibilities, spheroidal, aterms, out,
+                           lds);
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
     timeline_end(idg_debug_timeline_gridder);
 #endif
@@ -919,7 +996,7 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 //   workgroup returns at once.
 // queue: device.hpp queue_ints(nr_subgrids) ints of stream-ordered
 // workspace, its counters zeroed before the launches.
-template <int S_CT, int CB, int PT, bool FFT = false>
+template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     kernel_gridder_mirror_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -948,13 +1025,13 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
-  grid_mfma<S_CT, PT, CB, NW, true, FFT>(
+  grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds);
 }
 
-template <int S_CT, int CB, int PT, bool FFT = false>
+template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     kernel_gridder_general_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -987,7 +1064,8 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     const int s = all ? i : qv.at(i);
     const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
                                          image_size, w_step_in_lambda);
-    grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false, FFT>(
+    grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false, FFT,
+              PREC>(
         g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
         visibilities, spheroidal, aterms,
         subgrids + static_cast<size_t>(s) * 4 * npix, lds);
@@ -998,25 +1076,40 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
   }
 }
 
-#define IDG_GRIDDER(S_, PPT_, MODE_)                                     \
+// The MFMA kernels of one (S, FFT epilogue, precision): the combined
+// kernel (13-argument ABI) and the two-kernel form's mirror and general
+// kernels.
+struct GridderSet {
+  const void *combined, *mirror, *general;
+};
+template <int S_, int PPT_, bool FFT_, int PREC_>
+GridderSet gridder_set() {
+  return {reinterpret_cast<const void *>(
+              &kernel_gridder_mi355x<S_, PPT_, 16, 1, IDG_GRID_PT, FFT_, PREC_>),
+          reinterpret_cast<const void *>(
+              &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_>),
+          reinterpret_cast<const void *>(
+              &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_>)};
+}
+template <int S_, int PPT_, bool FFT_>
+GridderSet gridder_set_for(int prec) {
+  if constexpr (S_ == 32) {
+    switch (prec) {
+      case 0: return gridder_set<S_, PPT_, FFT_, 0>();
+      case kPrecTail | kPrecFlush:
+        return gridder_set<S_, PPT_, FFT_, kPrecTail | kPrecFlush>();
+      case kPrecFlush: return gridder_set<S_, PPT_, FFT_, kPrecFlush>();
+      default: return gridder_set<S_, PPT_, FFT_, kPrecTail>();
+    }
+  } else {
+    // no flush off S = 32 (the master needs a one-pass subgrid slot)
+    return (prec & kPrecTail) ? gridder_set<S_, PPT_, FFT_, kPrecTail>()
+                              : gridder_set<S_, PPT_, FFT_, 0>();
+  }
+}
+#define IDG_GRIDDER_VALU(S_, PPT_)                                        \
   reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mi355x<S_, PPT_, 16, MODE_, IDG_GRID_PT>)
-#define IDG_GRIDDER_MIRROR(S_, PPT_)                                      \
-  reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT>)
-#define IDG_GRIDDER_GENERAL(S_)                                           \
-  reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT>)
-// the FFT-epilogue instantiations (S = 32, MFMA only)
-#define IDG_GRIDDER_FFT32                                                 \
-  reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mi355x<32, 4, 16, 1, IDG_GRID_PT, true>)
-#define IDG_GRIDDER_MIRROR_FFT32                                          \
-  reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_mirror_mi355x<32, 16, IDG_GRID_PT, true>)
-#define IDG_GRIDDER_GENERAL_FFT32                                         \
-  reinterpret_cast<const void *>(                                         \
-      &kernel_gridder_general_mi355x<32, 16, IDG_GRID_PT, true>)
+      &kernel_gridder_mi355x<S_, PPT_, 16, 0, IDG_GRID_PT>)
 
 // IDG_GRID_SPLIT=0: the device entries launch the one combined MFMA kernel
 // (A/B of the two-launch form).
@@ -1035,43 +1128,40 @@ KernelChoice select_gridder(const Problem &p) {
   k.grid = p.nr_subgrids;
   const bool mfma = gridder_impl() == 1;
   k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
-  const void *part[2] = {nullptr, nullptr};
+  k.prec = precision_for(Direction::kGridder, p);
   // the FFT in the gridder's epilogue (S = 32, MFMA; IDG_GRID_FFT=0: the
   // launch layer runs launch_subgrid_fft after the plain gridder instead)
   const char *fenv = std::getenv("IDG_GRID_FFT");
   const bool fft_epilogue = p.fft_out && mfma && p.subgrid_size == 32 &&
                             !(fenv != nullptr && fenv[0] == '0');
+  GridderSet set{};
   switch (p.subgrid_size) {
     case 32:
-      k.func = mfma ? IDG_GRIDDER(32, 4, 1) : IDG_GRIDDER(32, 4, 0);
-      k.name = mfma ? "gridder_mi355x_s32" : "gridder_mi355x_s32_valu";
-      part[0] = IDG_GRIDDER_MIRROR(32, 4);
-      part[1] = IDG_GRIDDER_GENERAL(32);
-      if (fft_epilogue) {
-        k.func = IDG_GRIDDER_FFT32;
-        k.name = "gridder_fft_mi355x_s32";
-        part[0] = IDG_GRIDDER_MIRROR_FFT32;
-        part[1] = IDG_GRIDDER_GENERAL_FFT32;
-        k.fft_in_kernel = true;
-      }
+      set = fft_epilogue ? gridder_set_for<32, 4, true>(k.prec)
+                         : gridder_set_for<32, 4, false>(k.prec);
+      k.name = fft_epilogue ? "gridder_fft_mi355x_s32"
+                            : (mfma ? "gridder_mi355x_s32"
+                                    : "gridder_mi355x_s32_valu");
+      k.fft_in_kernel = fft_epilogue;
+      if (!mfma) set.combined = IDG_GRIDDER_VALU(32, 4);
       break;
     case 64:
-      k.func = mfma ? IDG_GRIDDER(64, 4, 1) : IDG_GRIDDER(64, 4, 0);
+      set = gridder_set_for<64, 4, false>(k.prec);
       k.name = mfma ? "gridder_mi355x_s64" : "gridder_mi355x_s64_valu";
-      part[0] = IDG_GRIDDER_MIRROR(64, 4);
-      part[1] = IDG_GRIDDER_GENERAL(64);
+      if (!mfma) set.combined = IDG_GRIDDER_VALU(64, 4);
       break;
     default:
-      k.func = mfma ? IDG_GRIDDER(0, 2, 1) : IDG_GRIDDER(0, 2, 0);
+      set = gridder_set_for<0, 2, false>(k.prec);
       k.name = mfma ? "gridder_mi355x_generic" : "gridder_mi355x_generic_valu";
       // odd S has no mirror pairs: one general-only launch
-      if (p.subgrid_size % 2 == 0) part[0] = IDG_GRIDDER_MIRROR(0, 2);
-      part[1] = IDG_GRIDDER_GENERAL(0);
+      if (p.subgrid_size % 2 != 0) set.mirror = nullptr;
+      if (!mfma) set.combined = IDG_GRIDDER_VALU(0, 2);
       break;
   }
+  k.func = set.combined;
   if (mfma && IDG_GRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
-    if (part[0]) k.parts[0] = {part[0], k.block, KernelChoice::kMirror};
-    k.parts[1] = {part[1], k.block, KernelChoice::kGeneral};
+    if (set.mirror) k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror};
+    k.parts[1] = {set.general, k.block, KernelChoice::kGeneral};
     // no subgrid mirror-eligible: the combined kernel, one workgroup per
     // subgrid (2.7 % faster on a w-term batch than the queue-fed kernel)
     k.all_general = {k.func, k.block, KernelChoice::kPlain};

@@ -230,6 +230,12 @@ bool two_kernel_form(int nr_subgrids) {
   return nr_subgrids >= kTwoKernelMinLaunch;
 }
 
+int precision_for(Direction dir, const Problem &p) {
+  if (const char *v = std::getenv("IDG_PREC")) return std::atoi(v) & 3;
+  (void)dir;
+  return kPrecTail | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
+}
+
 std::string validate(const Problem &p, const Extents &e,
                      const idg::Metadata *md) {
   std::ostringstream err;

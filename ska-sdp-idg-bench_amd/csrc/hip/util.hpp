@@ -119,6 +119,7 @@ struct KernelChoice {
   int block = 256;
   int grid = 0;  // = nr_subgrids
   bool fft_in_kernel = false;  // Problem::fft_out done by these kernels
+  int prec = 0;  // precision options of the MFMA kernels (device.hpp kPrec*)
   // The launch the device entries make instead, when parts[1] is set: one
   // kernel per subgrid class, each with the register allocation of its own
   // path.  parts[0] (kMirror; absent for odd S): grid =
@@ -155,6 +156,14 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
 // and tests; read per call).
 constexpr int kTwoKernelMinLaunch = 8192;
 bool two_kernel_form(int nr_subgrids);
+
+// Precision options (device.hpp kPrecTail | kPrecFlush) of the MFMA
+// kernels for a launch: the reduction-tail add where the coherent sums are
+// long enough for its 1e-6-rad phase error to show (more than
+// kTailMinChannels channels), blocked summation in the gridder likewise
+// (DESIGN.md §3.1, §3.3).  IDG_PREC=<0..3> forces the bits (A/B, tests).
+constexpr int kTailMinChannels = 16;
+int precision_for(Direction dir, const Problem &p);
 
 // Defined in the kernel TUs.
 KernelChoice select_gridder(const Problem &p);

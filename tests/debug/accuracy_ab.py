@@ -1,6 +1,7 @@
 """Debug aid (GPU box): the gridder's distance to exact accumulation for one
 library build (IDG_MI355X_LIB selects it), at the -c defaults and at
--c NR_CHANNELS=256 (T = 128).  Prints one JSON line per configuration:
+-c NR_CHANNELS=256 (T = 128).  Prints one JSON line per configuration and direction
+(IDG_PREC=<0..3> forces the kernels' precision options, util.hpp):
 ours_vs_exact / ref_vs_exact in the reference metric, plus the error of the
 largest pixels split into a coherent amplitude part (mean Re((o-e) e*)/|e|^2),
 a coherent phase part (the Im of the same) and the rest.  DESIGN.md §3.1.
@@ -25,6 +26,7 @@ CONFIGS = {"c_default": (2, 2, 128, 16), "c256": (2, 2, 128, 256)}
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else os.path.basename(
         os.environ.get("IDG_MI355X_LIB", "head"))
+    tag += f" IDG_PREC={os.environ.get('IDG_PREC', 'default')}"
     o = orc.Oracle()
     ref_lib = orc.Reference(portable=True) if orc.Reference.available(
         portable=True) else o
@@ -47,7 +49,7 @@ def main():
         big = np.abs(ec) > 0.25 * np.abs(ec).max()
         rel = ((oc - ec) * np.conj(ec))[big] / (np.abs(ec[big]) ** 2)
         rec = {
-            "tag": tag, "config": name,
+            "tag": tag, "config": name, "direction": "gridder",
             "ours_vs_exact": float(o.check_error(ours, e32)[0]),
             "ref_vs_exact": float(o.check_error(ref, e32)[0]),
             "ours_vs_ref": float(o.check_error(ours, ref)[0]),
@@ -57,6 +59,25 @@ def main():
             "big_rel_rms": float(np.sqrt(np.mean(np.abs(rel) ** 2))),
         }
         print(json.dumps(rec), flush=True)
+        # the degridder, on the reference's own degridder input subgrids
+        vo = np.zeros_like(a["visibilities"])
+        idg_amd.c_run_degridder(*args, a["uvw"], a["wavenumbers"], vo,
+                                a["spheroidal"], a["aterms"], a["metadata"],
+                                a["subgrids"])
+        vr = np.zeros_like(vo)
+        ref_lib.degridder(*args, a["uvw"], a["wavenumbers"], vr,
+                          a["spheroidal"], a["aterms"], a["metadata"],
+                          a["subgrids"])
+        vx = np.zeros(vo.shape, np.float64)
+        o.degridder_exact(*args, a["uvw"], a["wavenumbers"], vx,
+                          a["spheroidal"], a["aterms"], a["metadata"],
+                          a["subgrids"], nthreads=8)
+        vx32 = vx.astype(np.float32)
+        print(json.dumps({
+            "tag": tag, "config": name, "direction": "degridder",
+            "ours_vs_exact": float(o.check_error(vo, vx32)[0]),
+            "ref_vs_exact": float(o.check_error(vr, vx32)[0]),
+            "ours_vs_ref": float(o.check_error(vo, vr)[0])}), flush=True)
 
 
 if __name__ == "__main__":

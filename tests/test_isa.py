@@ -125,8 +125,10 @@ def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
             continue
         checked.append(k)
         assert total > 0 and drained == 0, (k, total, drained)
-    assert "gridder_mirror<32,16,4>" in checked, checked
-    assert "gridder_general<32,16,4>" in checked, checked
+    # every precision variant (the last template argument, device.hpp kPrec*)
+    for form in ("gridder_mirror<32,16,4,", "gridder_general<32,16,4,"):
+        for prec in ("0>", "1>", "3>"):
+            assert form + prec in checked, checked
 
 
 def test_lds_dma_m0_wait_state_checker():
@@ -150,3 +152,21 @@ def test_shipped_lds_dma_has_m0_wait_state(listings):
     assert res, "no kernel with an LDS-DMA"
     for name, total, _, _, m0 in res:
         assert total > 0 and m0 == 0, (name[:60], total, m0)
+
+
+def test_dpp_moves_of_vector_elements(tmp_path):
+    # hipcc (ROCm 7.2) emits one DPP move of element 0 for a loop of
+    # update_dpp over a float4's elements written inline (loop_form); the
+    # kernels go through device.hpp row_ror8 on named scalars (scalar_form),
+    # which must stay four moves (tests/probes/dpp_vector_probe.hip).
+    out = tmp_path / "dpp.s"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
+                    "-ffp-contract=off", "-I", os.path.join(PKG, "csrc"),
+                    "--cuda-device-only", "-S", "-o", str(out),
+                    os.path.join(REPO, "tests", "probes",
+                                 "dpp_vector_probe.hip")],
+                   check=True, capture_output=True, timeout=300)
+    text = out.read_text()
+    scalar = text[text.index("_Z11scalar_form"):]
+    scalar = scalar[:scalar.index("s_endpgm")]
+    assert scalar.count("row_ror:8") == 4
