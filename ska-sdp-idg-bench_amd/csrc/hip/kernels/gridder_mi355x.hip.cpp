@@ -58,6 +58,14 @@
 #ifndef IDG_GRID_FUSED_GENERAL
 #define IDG_GRID_FUSED_GENERAL 1
 #endif
+// K-steps on the f32 matrix core: bit u set runs channel quad u of every
+// 16-channel block on v_mfma_f32_16x16x4_f32 with the unsplit f32 phasor
+// and visibility (4 MFMAs per tile pair and channel), the others on the
+// f16 split (the split is ~40% of the VALU issue while the
+// matrix pipe is ~84% idle)
+#ifndef IDG_GRID_F32MASK
+#define IDG_GRID_F32MASK 0
+#endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW
 #define IDG_GRID_NW 8
@@ -256,7 +264,16 @@ struct MfmaLds {
   static constexpr int kSlotOff = kRedOff + 8;   // 2 fill maxima (bits)
   static constexpr int kSinkOff = kSlotOff + 2;  // 64 words: prefetch sink
   static constexpr int kWords = kSinkOff + 64;
+  // general path at S = 32 (kGeoLds): the subgrid's pixel geometry, l by
+  // column and m by row (32 each), then n and phase_offset per pixel
+  static constexpr int kGeoOff = kWords;
+  static constexpr int kWordsGeo = kGeoOff + 64 + 2 * 1024;
 };
+// LDS words of a kernel that runs grid_mfma's general path at S_CT
+template <int S_CT, int NW, int AT>
+constexpr int general_lds_words() {
+  return S_CT == 32 ? MfmaLds<AT, NW>::kWordsGeo : MfmaLds<AT, NW>::kWords;
+}
 
 // LDS-DMA of 4 bytes per lane from the lane's global address into
 // lds_dst + 4 * lane (lds_dst wave-uniform), as inline asm: the gridder uses
@@ -323,6 +340,17 @@ __device__ __forceinline__ void grid_mfma(
   constexpr bool kFused = !MIRROR && IDG_GRID_FUSED_GENERAL;
   constexpr int AT = kFused ? PT : 2 * PT;  // accumulator tiles per wave
   using Lds = MfmaLds<AT, NW>;
+  // channel quads on the f32 matrix core (mirror path; the general path's
+  // registers are full)
+  constexpr int kF32Mask = MIRROR ? IDG_GRID_F32MASK : 0;
+  // General path at S = 32: the pixel geometry lives in LDS, not in 32
+  // VGPRs across the whole subgrid (the general path's spills).  A lane's
+  // tile pair h covers pixels b0 = (wave PT + 2h) 16 + col and b0 + 16: l
+  // by column col and col + 16 for every pair, m wave-uniform per pair
+  // (row wave PT / 2 + h), n and phase_offset read per pair and timestep
+  // quad.
+  constexpr bool kGeoLds = kFused && S_CT == 32;
+  float *geo = reinterpret_cast<float *>(lds + Lds::kGeoOff);
   const int nt = g.nr_timesteps;
   const int nchq = (C + 3) / 4;  // channel quads
   const int nquads = (nt + 3) / 4;
@@ -377,15 +405,28 @@ __device__ __forceinline__ void grid_mfma(
     static_assert(PT % 2 == 0, "phases are packed over tile pairs");
     constexpr int PH = PT / 2;
     floatx2 L2[PH], M2[PH], N2[PH], PG2[PH];
+    if constexpr (kGeoLds) {
+      static_assert(PT == 8 && NW == 8, "one S = 32 pass: 1,024 pixels");
+      // (read after the first fill's barrier)
+      for (int p = tid; p < 1024; p += NW * 64) {
+        float l, m, n, pg;
+        pixel_geometry<true>(p, 32, image_size, g, l, m, n, pg);
+        geo[64 + p] = n;
+        geo[64 + 1024 + p] = pg;
+        if (p < 32) geo[p] = l;
+        if (p % 32 == 0) geo[32 + p / 32] = m;
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
-      float l, m, n, pg;
-      pixel_geometry<!MIRROR>(b, S, image_size, g, l, m, n, pg);
-      L2[i / 2][i % 2] = l;
-      M2[i / 2][i % 2] = m;
-      N2[i / 2][i % 2] = n;
-      PG2[i / 2][i % 2] = pg;
+      for (int i = 0; i < PT; ++i) {
+        const int b = min(gbase + (wave * PT + i) * 16 + col, half - 1);
+        float l, m, n, pg;
+        pixel_geometry<!MIRROR>(b, S, image_size, g, l, m, n, pg);
+        L2[i / 2][i % 2] = l;
+        M2[i / 2][i % 2] = m;
+        N2[i / 2][i % 2] = n;
+        PG2[i / 2][i % 2] = pg;
+      }
     }
     constexpr int PY = kFused ? 1 : PT;  // separate Y tiles (mirror path)
     floatx4 accx[PT], accy[PY];
@@ -491,10 +532,23 @@ __device__ __forceinline__ void grid_mfma(
                 bs[u] = rs * sc_s;
               }
             }
+            const bool f32ks = (kF32Mask >> (jj & 3)) & 1;
             jj += NW;
             while (jj >= nj) {
               jj -= nj;
               ++qq;
+            }
+            if (f32ks) {
+              // f32 K-step: the scaled values themselves in the hi columns,
+              // zero in the lo columns (the epilogue's hi + lo sum is kept)
+              const bool lo = (col & 8) != 0;
+              bbuf[(ks * 64 + lane) * 2] = make_uint4(
+                  lo ? 0u : __float_as_uint(bc[0]), lo ? 0u : __float_as_uint(bc[1]),
+                  lo ? 0u : __float_as_uint(bc[2]), lo ? 0u : __float_as_uint(bc[3]));
+              bbuf[(ks * 64 + lane) * 2 + 1] = make_uint4(
+                  lo ? 0u : __float_as_uint(bs[0]), lo ? 0u : __float_as_uint(bs[1]),
+                  lo ? 0u : __float_as_uint(bs[2]), lo ? 0u : __float_as_uint(bs[3]));
+              continue;
             }
             const unsigned xc = split_part(bc[0], bc[1], bpart);
             const unsigned yc = split_part(bc[2], bc[3], bpart);
@@ -589,6 +643,14 @@ __device__ __forceinline__ void grid_mfma(
               // and each K-step's B fragments are re-read from LDS per pair.
 #pragma unroll
               for (int h = 0; h < PH; ++h) {
+                if constexpr (kGeoLds) {
+                  const int b0 = (wave * PT + 2 * h) * 16 + col;
+                  L2[h] = floatx2{geo[col], geo[col + 16]};
+                  const float mh = geo[32 + wave * (PT / 2) + h];
+                  M2[h] = floatx2{mh, mh};
+                  N2[h] = floatx2{geo[64 + b0], geo[64 + b0 + 16]};
+                  PG2[h] = floatx2{geo[64 + 1024 + b0], geo[64 + 1024 + b0 + 16]};
+                }
                 floatx2 pidx = __builtin_elementwise_fma(cu, L2[h], cv * M2[h]);
                 pidx = __builtin_elementwise_fma(floatx2{c.w, c.w}, N2[h], pidx);
                 const floatx2 np = -pidx;
@@ -662,6 +724,38 @@ __device__ __forceinline__ void grid_mfma(
               const int ks = qq * nj + jj;
               const uint4 bx = bbuf[(ks * 64 + lane) * 2];
               const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
+              if ((kF32Mask >> u) & 1) {
+                // f32 K-step: per channel one f32 MFMA per tile and X/Y (K =
+                // the 4 timesteps of the lane groups; B = the scaled f32
+                // values, zero in the lo columns)
+                const float bc[4] = {__uint_as_float(bx.x), __uint_as_float(bx.y),
+                                     __uint_as_float(bx.z), __uint_as_float(bx.w)};
+                const float bs[4] = {__uint_as_float(by.x), __uint_as_float(by.y),
+                                     __uint_as_float(by.z), __uint_as_float(by.w)};
+#pragma unroll
+                for (int h = 0; h < PH; ++h) {
+                  float snx[4], csx[4], sny[4], csy[4];
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) {
+                    const float kj = kb[4 * u + j];
+                    const floatx2 ph =
+                        __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
+                    floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
+                    if constexpr ((PREC & kPrecTail) != 0) r = r + CR[h];
+                    sincos_rev(r.x, &snx[j], &csx[j]);
+                    sincos_rev(r.y, &sny[j], &csy[j]);
+                  }
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) {
+                    accx[2 * h] = mfma4(csx[j], bc[j], accx[2 * h]);
+                    accy[2 * h] = mfma4(snx[j], bs[j], accy[2 * h]);
+                    accx[2 * h + 1] = mfma4(csy[j], bc[j], accx[2 * h + 1]);
+                    accy[2 * h + 1] = mfma4(sny[j], bs[j], accy[2 * h + 1]);
+                  }
+                }
+                IDG_KSTEP_FENCE();
+                continue;
+              }
               const half8 bfx = pack4(bx.x, bx.y, bx.z, bx.w);
               const half8 bfy = pack4(by.x, by.y, by.z, by.w);
 #pragma unroll
@@ -892,7 +986,7 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
   if constexpr (MODE == 1) {
     constexpr int NW = IDG_GRID_NW;
     // both paths hold 2 PT accumulator tiles per wave
-    __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+    __shared__ unsigned lds[general_lds_words<S_CT, NW, 2 * PT>()];
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
     timeline_start(idg_debug_timeline_gridder);
 #endif
@@ -1045,7 +1139,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
         float2 *__restrict__ subgrids, int *__restrict__ queue,
         int nr_subgrids, int all) {
   constexpr int NW = IDG_GRID_NW;
-  __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+  __shared__ unsigned lds[general_lds_words<S_CT, NW, 2 * PT>()];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
   const int tid = threadIdx.x;

@@ -146,5 +146,11 @@ __device__ __forceinline__ floatx4 mfma16(const half8 &a, const half8 &b,
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x4_f32: A[row = lane % 16][k = lane / 16] = a,
+// B[k = lane / 16][col = lane % 16] = b; C as the f16 form (lane % 16 =
+// column, rows 4 (lane / 16) .. +3).  Exact f32 products and sums.
+__device__ __forceinline__ floatx4 mfma4(float a, float b, const floatx4 &c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 }  // namespace idg_mi355x

@@ -26,7 +26,14 @@ using namespace idg_mi355x;
 #endif
 enum { LDSB = 1, SMALL = 2, ANCH = 4 };
 
-template <int F>
+// FR of every 4 K-steps run on v_mfma_f32_16x16x4_f32 with the unsplit f32
+// cos/sin (one MFMA per tile, channel and X/Y: 32 per K-step and wave against
+// 8 f16 MFMAs; the B columns 8..15 of the f32 form are unused), the rest on
+// the f16 split (the matrix pipe is ~84% idle while the
+// split is ~40% of the VALU issue).
+// (mfma4: mfma.hpp)
+
+template <int F, int FR = 0>
 __global__ void __launch_bounds__(512, 4)
     kstep(float *out, const float *kin, const float4 *uvwin, int iters) {
   __shared__ uint4 bbuf[4 * 64 * 2];
@@ -45,6 +52,7 @@ __global__ void __launch_bounds__(512, 4)
   floatx4 accx[4], accy[4];
   for (int i = 0; i < 4; ++i) accx[i] = accy[i] = floatx4{0, 0, 0, 0};
   half8 bfx, bfy;
+  float b32x = lane * 1e-3f, b32y = lane * 2e-3f;
   for (int i = 0; i < 8; ++i) {
     bfx[i] = (_Float16)(lane * 1e-3f + i);
     bfy[i] = (_Float16)(i * 0.25f);
@@ -72,6 +80,34 @@ __global__ void __launch_bounds__(512, 4)
       const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
       bfx = pack4(bx.x, bx.y, bx.z, bx.w);
       bfy = pack4(by.x, by.y, by.z, by.w);
+      b32x = __builtin_bit_cast(float, bx.x);
+      b32y = __builtin_bit_cast(float, by.y);
+    }
+    if (FR > 0 && (it & 3) < FR) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float snx[4], csx[4], sny[4], csy[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float kj = kb[j];
+          const floatx2 ph =
+              __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
+          floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
+          sincos_rev(r.x, &snx[j], &csx[j]);
+          sincos_rev(r.y, &sny[j], &csy[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          accx[2 * h] = mfma4(csx[j], b32x, accx[2 * h]);
+          accy[2 * h] = mfma4(snx[j], b32y, accy[2 * h]);
+          accx[2 * h + 1] = mfma4(csy[j], b32x, accx[2 * h + 1]);
+          accy[2 * h + 1] = mfma4(sny[j], b32y, accy[2 * h + 1]);
+        }
+      }
+      IDG_KSTEP_FENCE();
+      NM[0] = NM[0] + floatx2{1.0f, 1.0f};
+      NM[1] = NM[1] - floatx2{1.0f, 1.0f};
+      continue;
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -109,15 +145,15 @@ __global__ void __launch_bounds__(512, 4)
   out[blockIdx.x * 512 + threadIdx.x] = r;
 }
 
-template <int F>
+template <int F, int FR = 0>
 void run(const char *name, float *out, const float *k, const float4 *uvw) {
   const int grid = 256 * WG_PER_CU, iters = 4000;
-  hipLaunchKernelGGL(kstep<F>, dim3(grid), dim3(512), 0, 0, out, k, uvw, 50);
+  hipLaunchKernelGGL((kstep<F, FR>), dim3(grid), dim3(512), 0, 0, out, k, uvw, 50);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, 0);
-  hipLaunchKernelGGL(kstep<F>, dim3(grid), dim3(512), 0, 0, out, k, uvw,
+  hipLaunchKernelGGL((kstep<F, FR>), dim3(grid), dim3(512), 0, 0, out, k, uvw,
                      iters);
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
@@ -147,6 +183,10 @@ int main() {
   run<LDSB>("B from LDS", out, k, uvw);
   run<LDSB | SMALL>("B from LDS, small rev", out, k, uvw);
   run<LDSB | ANCH>("B from LDS + anchors", out, k, uvw);
+  run<LDSB | ANCH, 1>("+ f32 MFMA on 1/4 of K-steps", out, k, uvw);
+  run<LDSB | ANCH, 2>("+ f32 MFMA on 2/4 of K-steps", out, k, uvw);
+  run<LDSB | ANCH, 3>("+ f32 MFMA on 3/4 of K-steps", out, k, uvw);
+  run<LDSB | ANCH, 4>("+ f32 MFMA on 4/4 of K-steps", out, k, uvw);
   (void)hipDeviceSynchronize();
   return 0;
 }
