@@ -765,6 +765,7 @@ __global__ void __launch_bounds__(512, IDG_DEGRID_WAVES)
     i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
     __syncthreads();
   }
+  if (tid == 0) queue_retire(queue);
 }
 
 // The general path alone, one 8-wave workgroup per subgrid with KP = 1,024

@@ -153,9 +153,13 @@ __device__ __forceinline__ int xcd_subgrid(int orig, int nwg) {
 // each), each a count on a 128-byte line of its own (a single count took
 // 0.28 ms of serialized atomics for 24,500 pushes) and a list; then one take
 // counter.  Layout in ints: counts at 32 x, take counter at kQueueNext,
-// shard x's list at kQueueHead + x * queue_cap(ns); ints [0, kQueueNext]
-// are zeroed before the launches.
-constexpr int kQueueShards = 8, kQueueNext = 256, kQueueHead = 288;
+// shard x's list at kQueueHead + x * queue_cap(ns); then the general
+// kernel's exit counter at kQueueExit.  The counters (ints [0, kQueueExit])
+// are zero before a launch pair: zeroed when the workspace is allocated, and
+// zeroed again by the general kernel's last workgroup to finish
+// (queue_retire), so a workspace cached per stream needs no clear per launch.
+constexpr int kQueueShards = 8, kQueueNext = 256, kQueueExit = 257,
+              kQueueHead = 288;
 
 __host__ __device__ inline int queue_cap(int ns) {
   return (ns + kQueueShards - 1) / kQueueShards;
@@ -182,6 +186,18 @@ struct QueueView {
     return q[kQueueHead + x * cap + (i - pre[x])];
   }
 };
+
+// Thread 0 of a general-kernel workgroup, after its last take: the last
+// workgroup of the grid to get here (every other one has read the counts
+// and made its last take) zeroes the counters for the next launch pair.
+__device__ __forceinline__ void queue_retire(int *queue) {
+  if (atomicAdd(queue + kQueueExit, 1) == static_cast<int>(gridDim.x) - 1) {
+#pragma unroll
+    for (int x = 0; x < kQueueShards; ++x) queue[32 * x] = 0;
+    queue[kQueueNext] = 0;
+    queue[kQueueExit] = 0;
+  }
+}
 
 __device__ __forceinline__ QueueView queue_view(const int *queue, int ns) {
   QueueView v;

@@ -58,14 +58,6 @@
 #ifndef IDG_GRID_FUSED_GENERAL
 #define IDG_GRID_FUSED_GENERAL 1
 #endif
-// K-steps on the f32 matrix core: bit u set runs channel quad u of every
-// 16-channel block on v_mfma_f32_16x16x4_f32 with the unsplit f32 phasor
-// and visibility (4 MFMAs per tile pair and channel), the others on the
-// f16 split (the split is ~40% of the VALU issue while the
-// matrix pipe is ~84% idle)
-#ifndef IDG_GRID_F32MASK
-#define IDG_GRID_F32MASK 0
-#endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW
 #define IDG_GRID_NW 8
@@ -340,9 +332,6 @@ __device__ __forceinline__ void grid_mfma(
   constexpr bool kFused = !MIRROR && IDG_GRID_FUSED_GENERAL;
   constexpr int AT = kFused ? PT : 2 * PT;  // accumulator tiles per wave
   using Lds = MfmaLds<AT, NW>;
-  // channel quads on the f32 matrix core (mirror path; the general path's
-  // registers are full)
-  constexpr int kF32Mask = MIRROR ? IDG_GRID_F32MASK : 0;
   // General path at S = 32: the pixel geometry lives in LDS, not in 32
   // VGPRs across the whole subgrid (the general path's spills).  A lane's
   // tile pair h covers pixels b0 = (wave PT + 2h) 16 + col and b0 + 16: l
@@ -532,23 +521,10 @@ __device__ __forceinline__ void grid_mfma(
                 bs[u] = rs * sc_s;
               }
             }
-            const bool f32ks = (kF32Mask >> (jj & 3)) & 1;
             jj += NW;
             while (jj >= nj) {
               jj -= nj;
               ++qq;
-            }
-            if (f32ks) {
-              // f32 K-step: the scaled values themselves in the hi columns,
-              // zero in the lo columns (the epilogue's hi + lo sum is kept)
-              const bool lo = (col & 8) != 0;
-              bbuf[(ks * 64 + lane) * 2] = make_uint4(
-                  lo ? 0u : __float_as_uint(bc[0]), lo ? 0u : __float_as_uint(bc[1]),
-                  lo ? 0u : __float_as_uint(bc[2]), lo ? 0u : __float_as_uint(bc[3]));
-              bbuf[(ks * 64 + lane) * 2 + 1] = make_uint4(
-                  lo ? 0u : __float_as_uint(bs[0]), lo ? 0u : __float_as_uint(bs[1]),
-                  lo ? 0u : __float_as_uint(bs[2]), lo ? 0u : __float_as_uint(bs[3]));
-              continue;
             }
             const unsigned xc = split_part(bc[0], bc[1], bpart);
             const unsigned yc = split_part(bc[2], bc[3], bpart);
@@ -724,38 +700,6 @@ __device__ __forceinline__ void grid_mfma(
               const int ks = qq * nj + jj;
               const uint4 bx = bbuf[(ks * 64 + lane) * 2];
               const uint4 by = bbuf[(ks * 64 + lane) * 2 + 1];
-              if ((kF32Mask >> u) & 1) {
-                // f32 K-step: per channel one f32 MFMA per tile and X/Y (K =
-                // the 4 timesteps of the lane groups; B = the scaled f32
-                // values, zero in the lo columns)
-                const float bc[4] = {__uint_as_float(bx.x), __uint_as_float(bx.y),
-                                     __uint_as_float(bx.z), __uint_as_float(bx.w)};
-                const float bs[4] = {__uint_as_float(by.x), __uint_as_float(by.y),
-                                     __uint_as_float(by.z), __uint_as_float(by.w)};
-#pragma unroll
-                for (int h = 0; h < PH; ++h) {
-                  float snx[4], csx[4], sny[4], csy[4];
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) {
-                    const float kj = kb[4 * u + j];
-                    const floatx2 ph =
-                        __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
-                    floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
-                    if constexpr ((PREC & kPrecTail) != 0) r = r + CR[h];
-                    sincos_rev(r.x, &snx[j], &csx[j]);
-                    sincos_rev(r.y, &sny[j], &csy[j]);
-                  }
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) {
-                    accx[2 * h] = mfma4(csx[j], bc[j], accx[2 * h]);
-                    accy[2 * h] = mfma4(snx[j], bs[j], accy[2 * h]);
-                    accx[2 * h + 1] = mfma4(csy[j], bc[j], accx[2 * h + 1]);
-                    accy[2 * h + 1] = mfma4(sny[j], bs[j], accy[2 * h + 1]);
-                  }
-                }
-                IDG_KSTEP_FENCE();
-                continue;
-              }
               const half8 bfx = pack4(bx.x, bx.y, bx.z, bx.w);
               const half8 bfy = pack4(by.x, by.y, by.z, by.w);
 #pragma unroll
@@ -1168,6 +1112,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     i = static_cast<int>(__builtin_amdgcn_readfirstlane(lds[0]));
     __syncthreads();
   }
+  if (tid == 0) queue_retire(queue);
 }
 
 // The MFMA kernels of one (S, FFT epilogue, precision): the combined

@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "../util.hpp"
 #include "common/types.hpp"
@@ -963,6 +965,25 @@ struct HomeSort {
   int4 *order = nullptr;  // entries {s, x, y, z or -1}
 };
 
+// Dynamic LDS per workgroup the current device grants (cached per device):
+// the LDS form of the home sort needs 2 x 4 nkeys bytes (kernel_home_place),
+// sized for gfx950's 160 KB; a part with less takes the multi-kernel form.
+size_t device_lds_per_block() {
+  static std::mutex mu;
+  static std::map<int, size_t> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock,
+                            dev) != hipSuccess)
+    v = 0;
+  cache[dev] = static_cast<size_t>(v);
+  return cache[dev];
+}
+
 hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
                      hipStream_t stream, HomeSort *hs) {
   const TileGrid tg(G);
@@ -970,7 +991,8 @@ hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
   // IDG_HOME_SORT=multi forces the multi-kernel form (tests)
   const char *form = std::getenv("IDG_HOME_SORT");
   const bool multi = (form != nullptr && std::strcmp(form, "multi") == 0) ||
-                     nkeys > kSortLdsKeys;
+                     nkeys > kSortLdsKeys ||
+                     2 * nkeys * sizeof(int) > device_lds_per_block();
   const int nwg = std::min(kSortMaxChunks, (ns + 3071) / 3072);
   const int chunk = (ns + nwg - 1) / nwg;
   const size_t ints =
@@ -1077,7 +1099,17 @@ hipError_t launch_splitter_fft(int nr_subgrids, int grid_size,
   const float scale = 1.0f / static_cast<float>(S * S);
   // IDG_SPLIT_FFT=0: the two launches (A/B and tests)
   const char *env = std::getenv("IDG_SPLIT_FFT");
-  if ((S != 32 && S != 64) || (env != nullptr && env[0] == '0')) {
+  // the fused kernel's static LDS (S = 64: ~66.5 KB, sized for gfx950's
+  // 160 KB) against what the device grants a workgroup
+  bool fits = true;
+  if (S == 32 || S == 64) {
+    hipFuncAttributes fa{};
+    const void *f = S == 32 ? reinterpret_cast<const void *>(&kernel_splitter_fft<32>)
+                            : reinterpret_cast<const void *>(&kernel_splitter_fft<64>);
+    fits = hipFuncGetAttributes(&fa, f) == hipSuccess &&
+           fa.sharedSizeBytes <= device_lds_per_block();
+  }
+  if ((S != 32 && S != 64) || !fits || (env != nullptr && env[0] == '0')) {
     const hipError_t err =
         launch_splitter(nr_subgrids, grid_size, S, nr_w_layers, d_metadata,
                         d_grid, d_subgrids, stream);

@@ -331,6 +331,75 @@ int resident_workgroups(const void *func, int block) {
   return n;
 }
 
+// The two-kernel form's queue workspace, cached per (device, stream): one
+// stream-ordered allocation per stream (grown when a launch needs more), its
+// counters zeroed when it is allocated or after a launch pair that did not
+// complete, and otherwise left zeroed by the general kernel itself -- so a
+// launch pair costs no allocation, clear or free.
+namespace {
+struct QueueSlot {
+  int *ptr = nullptr;
+  size_t ints = 0;
+  bool clean = false;
+  bool busy = false;
+};
+std::mutex g_queue_mu;
+std::map<std::pair<int, hipStream_t>, QueueSlot> g_queues;
+}  // namespace
+
+hipError_t QueueLease::acquire(hipStream_t s, size_t ints) {
+  int dev = 0;
+  hipError_t err = hipGetDevice(&dev);
+  if (err != hipSuccess) return err;
+  std::lock_guard<std::mutex> lock(g_queue_mu);
+  QueueSlot &q = g_queues[std::make_pair(dev, s)];
+  if (q.busy) {
+    // another host thread is between the launches of a pair on this stream:
+    // a private workspace for this pair
+    private_ = true;
+    err = hipMallocAsync(reinterpret_cast<void **>(&queue), ints * sizeof(int), s);
+    if (err != hipSuccess) return err;
+    stream = s;
+    return hipMemsetAsync(queue, 0, (kQueueExit + 1) * sizeof(int), s);
+  }
+  if (q.ints < ints) {
+    if (q.ptr) {
+      err = hipFreeAsync(q.ptr, s);
+      if (err != hipSuccess) return err;
+      q.ptr = nullptr;
+      q.ints = 0;
+    }
+    err = hipMallocAsync(reinterpret_cast<void **>(&q.ptr), ints * sizeof(int), s);
+    if (err != hipSuccess) return err;
+    q.ints = ints;
+    q.clean = false;
+  }
+  if (!q.clean) {
+    err = hipMemsetAsync(q.ptr, 0, (kQueueExit + 1) * sizeof(int), s);
+    if (err != hipSuccess) return err;
+  }
+  q.busy = true;
+  q.clean = false;
+  queue = q.ptr;
+  stream = s;
+  dev_ = dev;
+  return hipSuccess;
+}
+
+void QueueLease::release_clean() { clean_ = true; }
+
+QueueLease::~QueueLease() {
+  if (queue == nullptr) return;
+  if (private_) {
+    (void)hipFreeAsync(queue, stream);
+    return;
+  }
+  std::lock_guard<std::mutex> lock(g_queue_mu);
+  QueueSlot &q = g_queues[std::make_pair(dev_, stream)];
+  q.busy = false;
+  q.clean = clean_;
+}
+
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                         bool all_general, hipStream_t stream) {
   if (nr_subgrids <= 0) return hipSuccess;
@@ -340,12 +409,10 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                            dim3(k.all_general.block), args13, 0, stream);
   const int resident = resident_workgroups(general.func, general.block);
   if (resident <= 0) return hipErrorInvalidConfiguration;
-  int *queue = nullptr;
-  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&queue),
-                                  queue_ints(nr_subgrids) * sizeof(int),
-                                  stream);
+  QueueLease lease;
+  hipError_t err = lease.acquire(stream, queue_ints(nr_subgrids));
   if (err != hipSuccess) return err;
-  err = hipMemsetAsync(queue, 0, (kQueueNext + 1) * sizeof(int), stream);
+  int *queue = lease.queue;
   const bool run_mirror = mirror.func != nullptr && !all_general;
   int ns = nr_subgrids, all = run_mirror ? 0 : 1;
   void *args[16];
@@ -359,8 +426,10 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
   if (err == hipSuccess)
     err = hipLaunchKernel(general.func, dim3(std::min(nr_subgrids, resident)),
                           dim3(general.block), args, 0, stream);
-  const hipError_t ferr = hipFreeAsync(queue, stream);
-  return err != hipSuccess ? err : ferr;
+  // the general kernel's last workgroup zeroes the counters (device.hpp
+  // queue_retire); after a failed launch they are cleared on the next use
+  if (err == hipSuccess) lease.release_clean();
+  return err;
 }
 
 namespace {

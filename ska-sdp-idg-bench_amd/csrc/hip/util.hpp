@@ -146,6 +146,23 @@ struct KernelChoice {
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                         bool all_general, hipStream_t stream);
 
+// The queue workspace of one launch pair on `stream` (util.cpp): the
+// stream's cached workspace, counters zero, or -- while another host thread
+// holds that one -- a private stream-ordered allocation freed after the
+// pair.  release_clean(): the pair was launched whole, so the general
+// kernel leaves the counters zeroed.
+struct QueueLease {
+  int *queue = nullptr;
+  hipStream_t stream = nullptr;
+  hipError_t acquire(hipStream_t s, size_t ints);
+  void release_clean();
+  ~QueueLease();
+
+ private:
+  int dev_ = 0;
+  bool private_ = false, clean_ = false;
+};
+
 // Whether the device entries launch the two-kernel form (mirror kernel +
 // queue-fed general kernel) or the one combined kernel: the two-kernel form
 // from kTwoKernelMinLaunch subgrids up.  Below that (the N >= 4 shards of

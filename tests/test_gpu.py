@@ -863,6 +863,30 @@ def test_two_kernel_launch_matches_combined_kernel(idg, full, full_w,
 
 
 
+@pytest.mark.parametrize("op", ["gridder", "degridder"])
+def test_queue_workspace_reused_across_launches(idg, full_mixed, op,
+                                                monkeypatch):
+    """The two-kernel form's queue is cached per stream and its counters are
+    zeroed by the general kernel's last workgroup (device.hpp queue_retire),
+    not cleared per launch: back-to-back split-form launches on a mixed batch
+    (a non-empty queue every time), with a smaller launch in between (the
+    cached workspace larger than needed) and a larger one after it, give the
+    same output bit for bit each time."""
+    import torch
+    p, a, dev = full_mixed
+    monkeypatch.setenv("IDG_KERNEL_FORM", "split")
+    run = ((lambda q: _dgrid(idg, q, dev, dev["visibilities"]))
+           if op == "gridder" else
+           (lambda q: _ddegrid(idg, q, dev, dev["subgrids"])))
+    first = run(p)
+    small = dict(p, nr_subgrids=max(1, p["nr_subgrids"] // 7))
+    run(small)
+    again = [run(p) for _ in range(3)]
+    torch.cuda.synchronize()
+    for out in again:
+        assert torch.equal(out, first)
+
+
 @pytest.mark.parametrize("form", ["combined", "split"])
 def test_degridder_4_and_8_wave_workgroups_bitwise_on_ragged_batches(
         idg, form, monkeypatch):
