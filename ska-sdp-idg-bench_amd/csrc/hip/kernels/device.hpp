@@ -67,9 +67,14 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
 
 // Precision options of the MFMA kernels (template PREC, chosen per launch by
 // util.cpp precision_for): kPrecTail adds tail_k_rev to every phasor's
-// revolutions; kPrecFlush (gridder, S = 32) sums the accumulator tiles into
-// an f32 master every kFlushFills fills (at most 32 K-steps each).
-constexpr int kPrecTail = 1, kPrecFlush = 2;
+// revolutions; kPrecTailAlt (gridder) adds 4 x tail_k_rev to the first
+// channel of every channel quad and nothing to the other three -- the same
+// correction summed over each quad, for a quarter of the adds: the gridder
+// sums over channels, so the +3c / -c pattern cancels in every coherent sum
+// to first order (tests/debug/tail_mean_emul.py); kPrecFlush
+// (gridder, S = 32) sums the accumulator tiles into an f32 master every
+// kFlushFills fills (at most 32 K-steps each).
+constexpr int kPrecTail = 1, kPrecFlush = 2, kPrecTailAlt = 4;
 constexpr int kFlushFills = 4;
 
 // exp(i * phase_offset * kPhaseTail), |angle| <= 1.4e-4: cos = 1 - a^2/2

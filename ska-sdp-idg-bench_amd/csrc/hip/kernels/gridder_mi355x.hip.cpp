@@ -330,6 +330,9 @@ __device__ __forceinline__ void grid_mfma(
   // wave holds twice the pixel tiles in the same accumulator registers and
   // the S = 32 subgrid is one pass (B built once per subgrid, not twice).
   constexpr bool kFused = !MIRROR && IDG_GRID_FUSED_GENERAL;
+  // the reduction tail on every phasor, or 4x on one channel per quad
+  constexpr bool kTailAlt = (PREC & kPrecTailAlt) != 0;
+  constexpr bool kTailAll = (PREC & kPrecTail) != 0 && !kTailAlt;
   constexpr int AT = kFused ? PT : 2 * PT;  // accumulator tiles per wave
   using Lds = MfmaLds<AT, NW>;
   // General path at S = 32: the pixel geometry lives in LDS, not in 32
@@ -637,7 +640,9 @@ __device__ __forceinline__ void grid_mfma(
                 // the k * phase_index part of the reduction's tail, at the
                 // block's first channel (device.hpp: kPhaseTail)
                 floatx2 cr = {0.0f, 0.0f};
-                if constexpr ((PREC & kPrecTail) != 0) cr = tail_k_rev(np, ka);
+                if constexpr (kTailAll) cr = tail_k_rev(np, ka);
+                if constexpr (kTailAlt)
+                  cr = tail_k_rev(np, 4.0f * ka);
 #pragma unroll
                 for (int u = 0; u < CB / 4; ++u) {
                   const int jj = jb + u;
@@ -654,7 +659,9 @@ __device__ __forceinline__ void grid_mfma(
                     const floatx2 ph =
                         __builtin_elementwise_fma(np, floatx2{kj, kj}, PG2[h]);
                     floatx2 r = __builtin_elementwise_fma(ph, ih, nm);
-                    if constexpr ((PREC & kPrecTail) != 0) r = r + cr;
+                    if constexpr (kTailAll) r = r + cr;
+                    if constexpr (kTailAlt)
+                      if (j == 0) r = r + cr;
                     sincos_rev(r.x, &snx[j], &csx[j]);
                     sincos_rev(r.y, &sny[j], &csy[j]);
                   }
@@ -690,8 +697,10 @@ __device__ __forceinline__ void grid_mfma(
               NM[h] = floatx2{-__builtin_rintf(t.x), -__builtin_rintf(t.y)};
               // the k * phase_index part of the reduction's tail at the
               // block's first channel (device.hpp: kPhaseTail)
-              if constexpr ((PREC & kPrecTail) != 0)
+              if constexpr (kTailAll)
                 CR[h] = tail_k_rev(NP[h], ka);
+              if constexpr (kTailAlt)
+                CR[h] = tail_k_rev(NP[h], 4.0f * ka);
             }
 #pragma unroll
             for (int u = 0; u < CB / 4; ++u) {
@@ -714,7 +723,9 @@ __device__ __forceinline__ void grid_mfma(
                   const floatx2 ph =
                       __builtin_elementwise_fma(NP[h], floatx2{kj, kj}, PG2[h]);
                   floatx2 r = __builtin_elementwise_fma(ph, ih, NM[h]);
-                  if constexpr ((PREC & kPrecTail) != 0) r = r + CR[h];
+                  if constexpr (kTailAll) r = r + CR[h];
+                  if constexpr (kTailAlt)
+                    if (j == 0) r = r + CR[h];
                   sincos_rev(r.x, &snx[j], &csx[j]);
                   sincos_rev(r.y, &sny[j], &csy[j]);
                 }
@@ -1132,16 +1143,23 @@ GridderSet gridder_set() {
 }
 template <int S_, int PPT_, bool FFT_>
 GridderSet gridder_set_for(int prec) {
+  // the alternating tail replaces the every-phasor one in the gridder (the
+  // degridder reads kPrecTail alone)
+  if (prec & kPrecTailAlt) prec &= ~kPrecTail;
   if constexpr (S_ == 32) {
     switch (prec) {
       case 0: return gridder_set<S_, PPT_, FFT_, 0>();
       case kPrecTail | kPrecFlush:
         return gridder_set<S_, PPT_, FFT_, kPrecTail | kPrecFlush>();
       case kPrecFlush: return gridder_set<S_, PPT_, FFT_, kPrecFlush>();
+      case kPrecTailAlt: return gridder_set<S_, PPT_, FFT_, kPrecTailAlt>();
+      case kPrecTailAlt | kPrecFlush:
+        return gridder_set<S_, PPT_, FFT_, kPrecTailAlt | kPrecFlush>();
       default: return gridder_set<S_, PPT_, FFT_, kPrecTail>();
     }
   } else {
     // no flush off S = 32 (the master needs a one-pass subgrid slot)
+    if (prec & kPrecTailAlt) return gridder_set<S_, PPT_, FFT_, kPrecTailAlt>();
     return (prec & kPrecTail) ? gridder_set<S_, PPT_, FFT_, kPrecTail>()
                               : gridder_set<S_, PPT_, FFT_, 0>();
   }

@@ -231,7 +231,7 @@ bool two_kernel_form(int nr_subgrids) {
 }
 
 int precision_for(Direction dir, const Problem &p) {
-  if (const char *v = std::getenv("IDG_PREC")) return std::atoi(v) & 3;
+  if (const char *v = std::getenv("IDG_PREC")) return std::atoi(v) & 7;
   (void)dir;
   return kPrecTail | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
 }

@@ -10,6 +10,10 @@ double) against exact accumulation of the reference's f32 phases.
             sum as one phasor exp(i tau (phase_offset - kbar pidx_bar)),
             kbar the mean wavenumber, pidx_bar the phase index at the
             subgrid's mean (u, v, w)
+  sparseN   the block's tail added to one channel quad in N (N x c on quads
+            q % N == 0, nothing on the others): the same sum of corrections
+            over the block, 1/N of the adds
+  altN      the same per channel: N x c on channels k % N == 0
 
     python tests/debug/tail_mean_emul.py [C] [T]
 DESIGN.md §3.3.
@@ -42,7 +46,8 @@ def main():
     at = a["aterms"].reshape(-1, 2, S, S, 4, 2)
     at = at[..., 0].astype(f64) + 1j * at[..., 1]
     sph = a["spheroidal"].reshape(npix).astype(f64)
-    models = ("none", "block", "mean")
+    models = ("none", "block", "mean", "sparse2", "sparse4", "alt2", "alt4",
+              "alt8", "alt16")
     outs = {x: np.zeros((ns, 4, S, S, 2), f32) for x in models + ("exact",)}
     for s in range(ns):
         md = a["metadata"][s]
@@ -65,13 +70,24 @@ def main():
             r0 = fma32(ph, IH, nm)
             cr = (-pidx[None, :] * (kb * IH_LO).astype(f32)[:, None]).astype(f32)
             rb = (r0 + cr).astype(f32)
-            for x, r in (("none", r0), ("block", rb), ("mean", r0)):
+            quad = (np.arange(C) // 4)[:, None]
+            rs2 = np.where(quad % 2 == 0, (r0 + (2 * cr).astype(f32)).astype(f32), r0)
+            rs4 = np.where(quad % 4 == 0, (r0 + (4 * cr).astype(f32)).astype(f32), r0)
+            ch = np.arange(C)[:, None]
+            ra2 = np.where(ch % 2 == 0, (r0 + (2 * cr).astype(f32)).astype(f32), r0)
+            ra4 = np.where(ch % 4 == 0, (r0 + (4 * cr).astype(f32)).astype(f32), r0)
+            for x, r in (("none", r0), ("block", rb), ("mean", r0),
+                         ("sparse2", rs2), ("sparse4", rs4), ("alt2", ra2),
+                         ("alt4", ra4),
+                         ("alt8", np.where(ch % 8 == 0, (r0 + (8 * cr).astype(f32)).astype(f32), r0)),
+                         ("alt16", np.where(ch % 16 == 0, (r0 + (16 * cr).astype(f32)).astype(f32), r0))):
                 P[x] += np.exp(2j * np.pi * r.astype(f64)).T @ V[t]
         tail = np.exp(1j * poff.astype(f64) * f64(TAIL))
         ubar, vbar = uvw[:, 0].astype(f64).mean(), uvw[:, 1].astype(f64).mean()
         pbar = ubar * l.astype(f64) + vbar * m.astype(f64)
         kbar = k.astype(f64).mean()
-        rot = {"none": tail, "block": tail,
+        rot = {"none": tail, "block": tail, "sparse2": tail, "sparse4": tail,
+               "alt2": tail, "alt4": tail, "alt8": tail, "alt16": tail,
                "mean": np.exp(1j * f64(TAIL) * (poff.astype(f64) - kbar * pbar))}
         a1 = at[int(md["aterm_index"]), int(md["station1"])].reshape(npix, 2, 2)
         a2 = at[int(md["aterm_index"]), int(md["station2"])].reshape(npix, 2, 2)

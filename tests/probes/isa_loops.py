@@ -7,7 +7,7 @@ from collections import Counter
 
 src = open(sys.argv[1]).read()
 pat = sys.argv[2]
-for f in re.split(r'\n(?=_Z\w+:\s*\n)', src):
+for f in re.split(r'\n(?=_Z\w+:)', src):
     name = f.split(':')[0].strip()
     if pat not in name:
         continue

@@ -513,6 +513,10 @@ def sample_split(idg, oracle_lib, p, a, samples, ours, tag):
         json.dump(out, f, indent=1)
     for r in rows:
         assert split_holds(r), r
+        # the 1e-5 bar against exact accumulation on every sample, which the
+        # reference's own output misses at T x C = 32,768
+        if T * p["nr_channels"] > 4096:
+            assert r["ours_vs_exact"] <= TOLERANCE, r
     return out
 
 

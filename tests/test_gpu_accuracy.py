@@ -161,3 +161,55 @@ def test_c256_default_timesteps_harness_verdict_and_error_split(
         assert harness["restated_harness"]["verdict"] == "PASSED"
     else:
         assert split_holds(split), fmt(split)
+        # and the bar itself against exact accumulation, which the
+        # reference's own output misses here (ref_vs_exact ~1.3e-5)
+        assert split["ours_vs_exact"] <= TOLERANCE, fmt(split)
+
+
+# The -c defaults (tests/gridder_common.cpp:54-60: NR_STATIONS=2,
+# NR_TIMESLOTS=2, NR_TIMESTEPS_SUBGRID=128, NR_CHANNELS=16): both outputs
+# must be at least as close to the exact accumulation of the reference's own
+# f32 phases as the reference's CPU output is.
+@pytest.mark.parametrize("direction", ["gridder", "degridder"])
+def test_c_defaults_closer_to_exact_than_the_reference(idg, oracle_lib,
+                                                       ref_cpu, direction):
+    st, ts, T, C, G, S = 2, 2, 128, 16, 1024, 32
+    a = idg.generate(st, ts, T, C, G, S, nthreads=8)
+    ns = a["metadata"].size
+    args = (ns, G, S, idg.IMAGE_SIZE, idg.W_STEP, C, st)
+    ref_name, ref_lib = ref_cpu
+    nt = _cpu_threads()
+    if direction == "gridder":
+        ours = np.zeros((ns, 4, S, S, 2), np.float32)
+        idg.c_run_gridder(*args, a["uvw"], a["wavenumbers"],
+                          a["visibilities"], a["spheroidal"], a["aterms"],
+                          a["metadata"], ours)
+        ref = np.zeros_like(ours)
+        ref_lib.gridder(*args, a["uvw"], a["wavenumbers"], a["visibilities"],
+                        a["spheroidal"], a["aterms"], a["metadata"], ref)
+        exact = np.zeros(ours.shape, np.float64)
+        oracle_lib.gridder_exact(*args, a["uvw"], a["wavenumbers"],
+                                 a["visibilities"], a["spheroidal"],
+                                 a["aterms"], a["metadata"], exact,
+                                 nthreads=nt)
+    else:
+        ours = np.zeros_like(a["visibilities"])
+        idg.c_run_degridder(*args, a["uvw"], a["wavenumbers"], ours,
+                            a["spheroidal"], a["aterms"], a["metadata"],
+                            a["subgrids"])
+        ref = np.zeros_like(ours)
+        ref_lib.degridder(*args, a["uvw"], a["wavenumbers"], ref,
+                          a["spheroidal"], a["aterms"], a["metadata"],
+                          a["subgrids"])
+        exact = np.zeros(ours.shape, np.float64)
+        oracle_lib.degridder_exact(*args, a["uvw"], a["wavenumbers"], exact,
+                                   a["spheroidal"], a["aterms"],
+                                   a["metadata"], a["subgrids"], nthreads=nt)
+    split = error_split(oracle_lib, ours, ref, exact)
+    _record(f"c_default_{direction}", {"config": "-c defaults",
+                                        "direction": direction,
+                                        "reference_cpu": ref_name,
+                                        "split": split})
+    print(f"{direction} -c defaults: {fmt(split)}")
+    assert split["ours_vs_ref"] <= TOLERANCE, fmt(split)
+    assert split["ours_vs_exact"] <= split["ref_vs_exact"], fmt(split)
