@@ -832,8 +832,10 @@ def main(argv=None):
     kernels = {}
     for name, t in (("gridder", t_grid), ("degridder", t_degrid)):
         kname = idg_amd.kernel_name(name, S, C)
+        pbits, pdesc = idg_amd.precision_options(name, S, C)
         kernels[name] = {
             "kernel": kname,
+            "precision": {"bits": pbits, "options": pdesc},
             "ms": round(t * 1e3, 4),
             "mvis_s_per_gpu": round(nvis_max / t / 1e6, 2),
             "tflops": round(flops / t / 1e12, 3),

@@ -144,6 +144,13 @@ int idg_host_chunk_plan(int nr_subgrids, const idg_metadata_t *metadata,
  * (direction 0 = gridder, 1 = degridder); for profiles and reports. */
 const char *idg_kernel_name(int direction, int subgrid_size, int nr_channels);
 
+/* Precision options of the kernels the launch entries select for this
+ * geometry (bit 0: the phase-reduction tail on every phasor, bit 1: blocked
+ * summation, bit 2: the tail on one channel per quad); the
+ * IDG_PREC environment variable overrides them.  No reference counterpart:
+ * the reference's kernels have a single precision path. */
+int idg_precision_options(int direction, int subgrid_size, int nr_channels);
+
 /* ---- perf entries ---------------------------------------------------------
  * Replace hip::p_run_gridder / hip::p_run_degridder (kernel TUs, e.g.
  * gridder_v1.hip.cpp:114-116 -> app/HIP/util.cpp:176-253 / :313-390): the

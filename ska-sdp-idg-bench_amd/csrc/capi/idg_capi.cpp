@@ -280,6 +280,14 @@ const char *idg_kernel_name(int direction, int subgrid_size, int nr_channels) {
                         : idg_mi355x::select_degridder(p).name;
 }
 
+int idg_precision_options(int direction, int subgrid_size, int nr_channels) {
+  idg_mi355x::Problem p;
+  p.subgrid_size = subgrid_size;
+  p.nr_channels = nr_channels;
+  return direction == 0 ? idg_mi355x::select_gridder(p).prec
+                        : idg_mi355x::select_degridder(p).prec;
+}
+
 double idg_p_run_gridder(void) {
   idg_mi355x::Problem p;
   p.subgrid_size = static_cast<int>(get_env_var("SUBGRID_SIZE", 32));

@@ -174,11 +174,12 @@ struct QueueLease {
 constexpr int kTwoKernelMinLaunch = 8192;
 bool two_kernel_form(int nr_subgrids);
 
-// Precision options (device.hpp kPrecTail | kPrecFlush) of the MFMA
-// kernels for a launch: the reduction-tail add where the coherent sums are
-// long enough for its 1e-6-rad phase error to show (more than
-// kTailMinChannels channels), blocked summation in the gridder likewise
-// (DESIGN.md §3.1, §3.3).  IDG_PREC=<0..3> forces the bits (A/B, tests).
+// Precision options (device.hpp kPrecTail | kPrecFlush | kPrecTailAlt) of
+// the MFMA kernels for a launch: the gridder takes
+// the reduction tail on one channel per quad (kPrecTailAlt) and, above
+// kTailMinChannels channels, blocked summation (kPrecFlush: C = 256 gridder
+// 8.4e-6 -> 2.0e-6 from exact accumulation); the degridder no tail.
+// IDG_PREC=<0..7> forces the bits for both directions (A/B, tests).
 constexpr int kTailMinChannels = 16;
 int precision_for(Direction dir, const Problem &p);
 

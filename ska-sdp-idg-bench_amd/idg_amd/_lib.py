@@ -38,6 +38,7 @@ SIGNATURES = {
     "idg_validate_metadata": (_I, [_I, _I, _I, _I, _Z, _Z, _P]),
     "idg_host_chunk_plan": (_I, [_I, _P, _Z, _P, _I]),
     "idg_kernel_name": (_S, [_I, _I, _I]),
+    "idg_precision_options": (_I, [_I, _I, _I]),
     "idg_p_run_gridder": (_D, []),
     "idg_p_run_degridder": (_D, []),
     "idg_print_device_info": (None, []),

@@ -460,6 +460,20 @@ def kernel_name(direction, subgrid_size, nr_channels):
     return lib.idg_kernel_name(d, subgrid_size, nr_channels).decode()
 
 
+PRECISION_BITS = {1: "reduction tail on every phasor",
+                  2: "blocked summation (f32 master every 4 fills)",
+                  4: "reduction tail on one channel per quad"}
+
+
+def precision_options(direction, subgrid_size, nr_channels):
+    """The selected kernels' precision options (include/idg_mi355x.h
+    idg_precision_options): (bits, description)."""
+    d = {"gridder": 0, "degridder": 1}.get(direction, direction)
+    bits = int(lib.idg_precision_options(d, subgrid_size, nr_channels))
+    desc = [v for k, v in PRECISION_BITS.items() if bits & k]
+    return bits, "; ".join(desc) if desc else "none"
+
+
 def flops_gridder(nr_channels, nr_timesteps, nr_subgrids, subgrid_size,
                   nr_correlations=NR_CORRELATIONS):
     """Reference work model (app/common/common.cpp:100-129); nr_timesteps is

@@ -879,13 +879,21 @@ def test_queue_workspace_reused_across_launches(idg, full_mixed, op,
     import torch
     p, a, dev = full_mixed
     monkeypatch.setenv("IDG_KERNEL_FORM", "split")
-    run = ((lambda q: _dgrid(idg, q, dev, dev["visibilities"]))
-           if op == "gridder" else
-           (lambda q: _ddegrid(idg, q, dev, dev["subgrids"])))
-    first = run(p)
-    small = dict(p, nr_subgrids=max(1, p["nr_subgrids"] // 7))
-    run(small)
-    again = [run(p) for _ in range(3)]
+    ns = p["nr_subgrids"]
+
+    def run(n):
+        q = dict(p, nr_subgrids=n)
+        md = dev["metadata"][:n]
+        if op == "gridder":
+            return _dgrid(idg, q, dev, dev["visibilities"], md)
+        out = torch.zeros_like(dev["visibilities"])
+        idg.degridder_launch(*_params(q), dev["uvw"], dev["wavenumbers"], out,
+                             dev["spheroidal"], dev["aterms"], md,
+                             dev["subgrids"][:n])
+        return out
+    first = run(ns)
+    run(max(1, ns // 7))
+    again = [run(ns) for _ in range(3)]
     torch.cuda.synchronize()
     for out in again:
         assert torch.equal(out, first)
