@@ -62,7 +62,12 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 97% of the MFMA loops' remaining VALU (v_cvt_pk_f16_f32 4.5, v_fma_mix_f32
 # 4.46, v_pk_fma_f32 4.8), f16 MFMA 4.7 beside the split that feeds it
 # (split_rates_probe.hip: split + 2 dependent MFMAs - split alone, per MFMA).
-ISSUE_CYC = {"trans": 8.35, "mfma_f16": 4.7, "other": 4.46}
+ISSUE_CYC = {"trans": 8.35, "mfma_f16": 4.7, "other": 4.46,
+             # per-class prices (round 4): v_cvt_pk_f16_f32; the FMA_F32
+             # class = v_fma_mix_f32 4.46 and v_pk_fma_f32 4.8 in the loops'
+             # 2:1 mix; plain f32 / integer VALU (v_fma_f32, v_add_f32,
+             # v_mov_b32: 2.5-2.7)
+             "cvt": 4.5, "fma_f32": 4.58, "plain": 2.6}
 MFMA_F16_FLOP = 16 * 16 * 32 * 2  # v_mfma_f32_16x16x32_f16
 NR_SIMDS = 1024
 
@@ -436,8 +441,18 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled,
         trans_i = ib["insts_trans"] * scale
         mfma = ib["insts_mfma_f16"] * scale
         other = ib["insts_valu"] * scale - trans_i - mfma
+        cls = ib.get("insts_class")
+        if cls:
+            # per VALU class (round 4, SQ_INSTS_VALU_CVT / _FMA_F32 passes):
+            # the f16-output converts and the mix / packed FMAs at their
+            # measured VOP3 costs, every other VALU at the plain f32 rate
+            other_cyc = (cls["SQ_INSTS_VALU_CVT"] * ISSUE_CYC["cvt"] +
+                         cls["SQ_INSTS_VALU_FMA_F32"] * ISSUE_CYC["fma_f32"] +
+                         cls["plain"] * ISSUE_CYC["plain"]) * scale
+        else:
+            other_cyc = other * ISSUE_CYC["other"]
         cyc = (trans_i * ISSUE_CYC["trans"] + mfma * ISSUE_CYC["mfma_f16"] +
-               other * ISSUE_CYC["other"]) / NR_SIMDS
+               other_cyc) / NR_SIMDS
         t_issue = cyc / CLOCK_HZ
         out["issue_efficiency"] = {
             "frac": round(t_issue / t, 4),

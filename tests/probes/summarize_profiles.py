@@ -29,6 +29,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(
     __file__))))
 ROCPD2CSV = "/opt/rocm/bin/rocpd2csv"
 CYC_TRANS, CYC_MFMA_F16, CYC_VALU = 8.35, 4.7, 4.46
+# Round 4: with the VALU class counters (pmc_sq.sh's optional passes) the
+# "other" VALU is priced per class: v_cvt_pk_f16_f32 (CVT) 4.5, the FMA_F32
+# class 4.58 (v_fma_mix_f32 4.46 and v_pk_fma_f32 4.8 in the loops' 2:1
+# mix, tests/probes/isa_loops.py), everything else at the plain f32 /
+# integer rate 2.6 (v_fma_f32, v_add_f32, v_mov_b32 2.5-2.7 in
+# instr_rates_probe.hip).
+CYC_CLASS = {"SQ_INSTS_VALU_CVT": 4.5, "SQ_INSTS_VALU_FMA_F32": 4.58}
+CYC_PLAIN = 2.6
 N_SIMD, N_XCD = 1024, 8
 
 
@@ -213,16 +221,29 @@ def main():
                                 "SQ_INSTS_VALU_MFMA_F16", "GRBM_GUI_ACTIVE")):
             other = (c["SQ_INSTS_VALU"] - c["SQ_INSTS_VALU_TRANS_F32"]
                      - c["SQ_INSTS_VALU_MFMA_F16"])
+            classed = all(k in c for k in CYC_CLASS)
+            if classed:
+                cls = {k: c[k] for k in CYC_CLASS}
+                plain = other - sum(cls.values())
+                other_cyc = (sum(c[k] * v for k, v in CYC_CLASS.items())
+                             + plain * CYC_PLAIN)
+                model = ("(trans x 8.35 + f16 MFMA x 4.7 + CVT x 4.5 + FMA_F32 "
+                         "x 4.58 + the rest x 2.6 cycles, tests/probes/"
+                         "instr_rates_probe.hip) / (GRBM_GUI_ACTIVE / 8 XCDs), "
+                         "summed over 1024 SIMDs")
+            else:
+                other_cyc = other * CYC_VALU
+                model = ("(trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46 "
+                         "cycles, tests/probes/instr_rates_probe.hip) / "
+                         "(GRBM_GUI_ACTIVE / 8 XCDs), summed over 1024 SIMDs")
             cyc = (c["SQ_INSTS_VALU_TRANS_F32"] * CYC_TRANS
                    + c["SQ_INSTS_VALU_MFMA_F16"] * CYC_MFMA_F16
-                   + other * CYC_VALU) / N_SIMD
+                   + other_cyc) / N_SIMD
             per_simd = c["GRBM_GUI_ACTIVE"] / N_XCD
             issue = {
                 "resource": "VALU issue per SIMD",
                 "utilization": round(cyc / per_simd, 3),
-                "model": ("(trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46 "
-                          "cycles, tests/probes/instr_rates_probe.hip) / "
-                          "(GRBM_GUI_ACTIVE / 8 XCDs), summed over 1024 SIMDs"),
+                "model": model,
                 "insts_valu": c["SQ_INSTS_VALU"],
                 "insts_trans": c["SQ_INSTS_VALU_TRANS_F32"],
                 "insts_mfma_f16": c["SQ_INSTS_VALU_MFMA_F16"],
@@ -230,6 +251,8 @@ def main():
                 "source": os.path.relpath(
                     os.path.join(args.out, "pmc_sq_summary.json"), REPO),
             }
+            if classed:
+                issue["insts_class"] = dict(cls, plain=plain)
             summary["issue_bound"][n] = issue
         entry = wl.setdefault(n, {})
         if hbm is not None:
