@@ -956,10 +956,13 @@ hipError_t launch_subgrid_fft(int nr_subgrids, int subgrid_size, int sign,
 
 namespace {
 
-// The home sort's stream-ordered workspace: hist (16 nkeys, LDS form) |
-// slot (2 ns) | offset (nkeys + 1) | order (ns) | count, cursor (nkeys each,
-// multi-kernel form).
+// The home sort's workspace (util.hpp WorkspaceLease, cached per stream
+// and held until the kernels that read it are enqueued): hist (16 nkeys,
+// LDS form) | slot (2 ns) | offset (nkeys + 1) | order (ns) | count,
+// cursor (nkeys each, multi-kernel form).  Every launch rewrites what it
+// reads.
 struct HomeSort {
+  WorkspaceLease lease;
   int *ws = nullptr;
   int *offset = nullptr;
   int4 *order = nullptr;  // entries {s, x, y, z or -1}
@@ -999,9 +1002,10 @@ hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
       static_cast<size_t>(nkeys) + 1 + 8 * static_cast<size_t>(ns) +
       (multi ? 2 * static_cast<size_t>(nkeys)
              : static_cast<size_t>(kSortMaxChunks) * nkeys);
-  hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&hs->ws),
-                                  ints * sizeof(int), stream);
+  hipError_t err =
+      hs->lease.acquire(stream, kWorkspaceHomeSort, ints * sizeof(int));
   if (err != hipSuccess) return err;
+  hs->ws = static_cast<int *>(hs->lease.ptr);
   // hist rows (64 B) first, then the 16-byte slot[] and order[] entries
   int *hist = hs->ws;
   int4 *slot = reinterpret_cast<int4 *>(
@@ -1032,11 +1036,13 @@ hipError_t home_sort(const idg::Metadata *md, int ns, int G, int S, int W,
   return hipGetLastError();
 }
 
+// (the lease returns the workspace to the stream's cache when `hs` goes
+// out of scope, after every kernel reading it is enqueued)
 hipError_t free_home_sort(const HomeSort &hs, hipError_t err,
                           hipStream_t stream) {
-  if (hs.ws == nullptr) return err;
-  const hipError_t ferr = hipFreeAsync(hs.ws, stream);
-  return err != hipSuccess ? err : ferr;
+  (void)hs;
+  (void)stream;
+  return err;
 }
 
 }  // namespace

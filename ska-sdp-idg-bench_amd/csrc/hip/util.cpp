@@ -11,6 +11,7 @@
 #include <memory>
 #include <sstream>
 #include <thread>
+#include <tuple>
 #include <utility>
 
 #include "lib-hip.hpp"
@@ -334,73 +335,67 @@ int resident_workgroups(const void *func, int block) {
   return n;
 }
 
-// The two-kernel form's queue workspace, cached per (device, stream): one
-// stream-ordered allocation per stream (grown when a launch needs more), its
-// counters zeroed when it is allocated or after a launch pair that did not
-// complete, and otherwise left zeroed by the general kernel itself -- so a
-// launch pair costs no allocation, clear or free.
+// Device workspaces cached per (device, stream, slot): one stream-ordered
+// allocation per stream and use (grown when a launch needs more), so the
+// launches that need one (the two-kernel form's queue, the pipeline's home
+// sort) make no allocation or free per call.  A slot is
+// leased for the enqueueing of one launch sequence; while another host
+// thread holds it, the caller gets a private allocation freed after its
+// sequence.
 namespace {
-struct QueueSlot {
-  int *ptr = nullptr;
-  size_t ints = 0;
+struct WorkspaceSlot {
+  void *ptr = nullptr;
+  size_t bytes = 0;
   bool clean = false;
   bool busy = false;
 };
-std::mutex g_queue_mu;
-std::map<std::pair<int, hipStream_t>, QueueSlot> g_queues;
+std::mutex g_ws_mu;
+std::map<std::tuple<int, hipStream_t, int>, WorkspaceSlot> g_ws;
 }  // namespace
 
-hipError_t QueueLease::acquire(hipStream_t s, size_t ints) {
+hipError_t WorkspaceLease::acquire(hipStream_t s, int slot, size_t bytes) {
   int dev = 0;
   hipError_t err = hipGetDevice(&dev);
   if (err != hipSuccess) return err;
-  std::lock_guard<std::mutex> lock(g_queue_mu);
-  QueueSlot &q = g_queues[std::make_pair(dev, s)];
-  if (q.busy) {
-    // another host thread is between the launches of a pair on this stream:
-    // a private workspace for this pair
-    private_ = true;
-    err = hipMallocAsync(reinterpret_cast<void **>(&queue), ints * sizeof(int), s);
-    if (err != hipSuccess) return err;
-    stream = s;
-    return hipMemsetAsync(queue, 0, (kQueueExit + 1) * sizeof(int), s);
-  }
-  if (q.ints < ints) {
-    if (q.ptr) {
-      err = hipFreeAsync(q.ptr, s);
-      if (err != hipSuccess) return err;
-      q.ptr = nullptr;
-      q.ints = 0;
-    }
-    err = hipMallocAsync(reinterpret_cast<void **>(&q.ptr), ints * sizeof(int), s);
-    if (err != hipSuccess) return err;
-    q.ints = ints;
-    q.clean = false;
-  }
-  if (!q.clean) {
-    err = hipMemsetAsync(q.ptr, 0, (kQueueExit + 1) * sizeof(int), s);
-    if (err != hipSuccess) return err;
-  }
-  q.busy = true;
-  q.clean = false;
-  queue = q.ptr;
   stream = s;
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  WorkspaceSlot &w = g_ws[std::make_tuple(dev, s, slot)];
+  if (w.busy) {
+    private_ = true;
+    clean = false;
+    return hipMallocAsync(&ptr, bytes, s);
+  }
+  if (w.bytes < bytes) {
+    if (w.ptr) {
+      err = hipFreeAsync(w.ptr, s);
+      if (err != hipSuccess) return err;
+      w.ptr = nullptr;
+      w.bytes = 0;
+    }
+    err = hipMallocAsync(&w.ptr, bytes, s);
+    if (err != hipSuccess) return err;
+    w.bytes = bytes;
+    w.clean = false;
+  }
+  w.busy = true;
+  clean = w.clean;
+  w.clean = false;
+  ptr = w.ptr;
   dev_ = dev;
+  slot_ = slot;
   return hipSuccess;
 }
 
-void QueueLease::release_clean() { clean_ = true; }
-
-QueueLease::~QueueLease() {
-  if (queue == nullptr) return;
+WorkspaceLease::~WorkspaceLease() {
+  if (ptr == nullptr) return;
   if (private_) {
-    (void)hipFreeAsync(queue, stream);
+    (void)hipFreeAsync(ptr, stream);
     return;
   }
-  std::lock_guard<std::mutex> lock(g_queue_mu);
-  QueueSlot &q = g_queues[std::make_pair(dev_, stream)];
-  q.busy = false;
-  q.clean = clean_;
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  WorkspaceSlot &w = g_ws[std::make_tuple(dev_, stream, slot_)];
+  w.busy = false;
+  w.clean = leave_clean;
 }
 
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
@@ -412,10 +407,18 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                            dim3(k.all_general.block), args13, 0, stream);
   const int resident = resident_workgroups(general.func, general.block);
   if (resident <= 0) return hipErrorInvalidConfiguration;
-  QueueLease lease;
-  hipError_t err = lease.acquire(stream, queue_ints(nr_subgrids));
+  // the queue's counters are zero when the workspace is new or the last
+  // pair did not complete, and left zero by the general kernel's last
+  // workgroup otherwise (device.hpp queue_retire)
+  WorkspaceLease lease;
+  hipError_t err = lease.acquire(stream, kWorkspaceQueue,
+                                 queue_ints(nr_subgrids) * sizeof(int));
   if (err != hipSuccess) return err;
-  int *queue = lease.queue;
+  int *queue = static_cast<int *>(lease.ptr);
+  if (!lease.clean) {
+    err = hipMemsetAsync(queue, 0, (kQueueExit + 1) * sizeof(int), stream);
+    if (err != hipSuccess) return err;
+  }
   const bool run_mirror = mirror.func != nullptr && !all_general;
   int ns = nr_subgrids, all = run_mirror ? 0 : 1;
   void *args[16];
@@ -431,7 +434,7 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                           dim3(general.block), args, 0, stream);
   // the general kernel's last workgroup zeroes the counters (device.hpp
   // queue_retire); after a failed launch they are cleared on the next use
-  if (err == hipSuccess) lease.release_clean();
+  lease.leave_clean = err == hipSuccess;
   return err;
 }
 

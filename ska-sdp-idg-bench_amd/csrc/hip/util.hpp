@@ -146,21 +146,24 @@ struct KernelChoice {
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
                         bool all_general, hipStream_t stream);
 
-// The queue workspace of one launch pair on `stream` (util.cpp): the
-// stream's cached workspace, counters zero, or -- while another host thread
-// holds that one -- a private stream-ordered allocation freed after the
-// pair.  release_clean(): the pair was launched whole, so the general
-// kernel leaves the counters zeroed.
-struct QueueLease {
-  int *queue = nullptr;
+// A device workspace cached per (device, stream, slot) (util.cpp), leased
+// for the enqueueing of one launch sequence on `stream`: ptr holds at least
+// the bytes asked for; `clean` = the last lease of this slot ended with
+// leave_clean set (its contents are what that sequence left).  While another
+// host thread holds the slot, ptr is a private stream-ordered allocation
+// (never clean) freed after the sequence.
+constexpr int kWorkspaceQueue = 0, kWorkspaceHomeSort = 1;
+struct WorkspaceLease {
+  void *ptr = nullptr;
   hipStream_t stream = nullptr;
-  hipError_t acquire(hipStream_t s, size_t ints);
-  void release_clean();
-  ~QueueLease();
+  bool clean = false;
+  bool leave_clean = false;
+  hipError_t acquire(hipStream_t s, int slot, size_t bytes);
+  ~WorkspaceLease();
 
  private:
-  int dev_ = 0;
-  bool private_ = false, clean_ = false;
+  int dev_ = 0, slot_ = 0;
+  bool private_ = false;
 };
 
 // Whether the device entries launch the two-kernel form (mirror kernel +
