@@ -103,6 +103,14 @@ def apply_wterms(w, a):
     a["metadata"]["z"] = rng.integers(0, w["w_layers"], a["metadata"].size)
 
 
+def progress(msg):
+    """One progress line on stderr (a long workload's phases: batch
+    generation, upload, timing, pipeline, CPU baseline), so a run that
+    takes minutes is seen to be alive."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr,
+          flush=True)
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -122,7 +130,9 @@ def parse(argv=None):
     ap.add_argument("--timeslots", type=int, default=None,
                     help="override NR_TIMESLOTS (batch size)")
     ap.add_argument("--cpu-sample-subgrids", type=int, default=128,
-                    help="subgrids per host thread in the cpu_baseline")
+                    help="subgrids per host thread in the cpu_baseline at "
+                         "C = 16, S = 32 (scaled to the same work for other "
+                         "C and S)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the FFT / adder / grid-sum / splitter")
@@ -265,9 +275,12 @@ def cpu_baseline(w, a, nsample):
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+    # the sample is sized for configs[1] (C = 16, S = 32: ~7 s on one core);
+    # other workloads take the same work per thread (c256: 8 subgrids, s64: 32)
+    nsample = max(8, nsample * 16 * 32 * 32 // (C * S * S))
     n = min(nsample, a["metadata"].size)
     md = a["metadata"][:n]
-    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
     args = (n, w["grid_size"], S, 0.01, w.get("w_step", 0.0), C,
             w["nr_stations"])
     if orc.Reference.available(portable=True):
@@ -817,6 +830,7 @@ def main(argv=None):
 
     # ---- synthetic batch (reference generators), this rank's part in HBM --
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    progress(f"generating the {args.workload} batch")
     a = make_batch(w, nthreads=threads)
     ns_total = a["metadata"].size
     idg_amd.validate_metadata(ns_total, S, C, w["nr_stations"], ns_total * T,
@@ -826,8 +840,10 @@ def main(argv=None):
     idg_amd.validate_metadata(nsub, S, C, w["nr_stations"],
                               part["row1"] - part["row0"],
                               w["nr_timeslots"], part["metadata"])
+    progress(f"uploading {nsub} subgrids")
     dev = upload(part)
     stream = torch.cuda.current_stream()
+    progress("timing")
 
     from idg_amd.energy import EnergyMeter
     meter = EnergyMeter(local_rank)
@@ -882,6 +898,7 @@ def main(argv=None):
     # ---- pipeline steps around the path (not in `value`) ----------------
     pipeline, grid_sum = None, None
     if not args.no_pipeline or args.dump:
+        progress("pipeline steps")
         pipeline, grid_sum = time_pipeline(w, dev, outs[0], stream,
                                            args.steps, world, dist)
         extra = sum(pipeline[k] for k in ("fft_ms", "adder_ms",
@@ -991,6 +1008,7 @@ def main(argv=None):
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(w, a, args.cpu_sample_subgrids)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -75,7 +75,10 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
 // (gridder, S = 32) sums the accumulator tiles into an f32 master every
 // kFlushFills fills (at most 32 K-steps each).
 constexpr int kPrecTail = 1, kPrecFlush = 2, kPrecTailAlt = 4;
-constexpr int kFlushFills = 4;
+#ifndef IDG_FLUSH_FILLS
+#define IDG_FLUSH_FILLS 4
+#endif
+constexpr int kFlushFills = IDG_FLUSH_FILLS;
 
 // exp(i * phase_offset * kPhaseTail), |angle| <= 1.4e-4: cos = 1 - a^2/2
 // (the a^4 term is below 1e-16), sin = a (the a^3 term below 5e-13).
