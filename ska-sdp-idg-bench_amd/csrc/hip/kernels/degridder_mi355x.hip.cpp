@@ -133,6 +133,10 @@ __device__ __forceinline__ void rotate_entry(float4 &pa, float4 &pb, float c,
 // Per phasor: 1 packed phase instruction, v_sin + v_cos, 3 split
 // instructions, half an MFMA.
 // ---------------------------------------------------------------------------
+#ifndef IDG_DEGRID_BSCALE
+#define IDG_DEGRID_BSCALE 0
+#endif
+
 template <int KP>
 struct DegridMfmaLds {
   static constexpr int kGeoWords = KP * 4;              // l | m | poff | n
@@ -312,7 +316,9 @@ __device__ __forceinline__ void degrid_mfma(
     }
   };
 
-  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range.
+  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range
+  // (below 2^IDG_DEGRID_BSCALE: high in the range keeps the split's lo part
+  // a normal f16 for all but the smallest pixels).
   auto scale_exp = [](float vmax) {
     int e = 0;
     if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
@@ -332,7 +338,7 @@ __device__ __forceinline__ void degrid_mfma(
     for (int h = 0; h < 2; ++h)
       v = fmaxf(v, fmaxf(absmax(k.pa[h], k.pb[h]), absmax(k.ma[h], k.mb[h])));
     e = scale_exp(2.0f * block_max(v));
-    if (has_block) store_block(tid, k, ldexpf(1.0f, -e));
+    if (has_block) store_block(tid, k, ldexpf(1.0f, IDG_DEGRID_BSCALE - e));
     __syncthreads();
   } else {
     float v = 0.0f;
@@ -344,7 +350,8 @@ __device__ __forceinline__ void degrid_mfma(
     }
     e = scale_exp(2.0f * block_max(v));
   }
-  const float scale = ldexpf(1.0f, -e), unscale = ldexpf(1.0f, e);
+  const float scale = ldexpf(1.0f, IDG_DEGRID_BSCALE - e),
+              unscale = ldexpf(1.0f, e - IDG_DEGRID_BSCALE);
   // B fragments and geometry of pairs [pc0, pc0 + KP): one thread per
   // K-block (2 pairs), writing all 16 column lanes of it.
   auto build = [&](int pc0) {

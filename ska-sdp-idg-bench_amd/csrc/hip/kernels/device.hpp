@@ -76,7 +76,7 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
 // kFlushFills fills (at most 32 K-steps each).
 constexpr int kPrecTail = 1, kPrecFlush = 2, kPrecTailAlt = 4;
 #ifndef IDG_FLUSH_FILLS
-#define IDG_FLUSH_FILLS 4
+#define IDG_FLUSH_FILLS 8
 #endif
 constexpr int kFlushFills = IDG_FLUSH_FILLS;
 

@@ -58,6 +58,11 @@
 #ifndef IDG_GRID_FUSED_GENERAL
 #define IDG_GRID_FUSED_GENERAL 1
 #endif
+// the B operand's (visibilities') power-of-two scale targets a first-fill
+// maximum in [2^(kBS-1), 2^kBS)
+#ifndef IDG_GRID_BSCALE
+#define IDG_GRID_BSCALE 0
+#endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW
 #define IDG_GRID_NW 8
@@ -377,10 +382,15 @@ __device__ __forceinline__ void grid_mfma(
 #pragma unroll
     for (int w = 0; w < NW; ++w) vmax = fmaxf(vmax, red[w]);
   }
+  // the scaled values sit below 2^kBS (IDG_GRID_BSCALE): high in f16 range,
+  // so the lo part of the split stays a normal f16 down to 2^(kBS-17) of
+  // the maximum instead of 2^-3 (f16 subnormals hold only 2^-24 absolute)
+  constexpr int kBS = IDG_GRID_BSCALE;
+  static_assert(kBS >= 0 && kBS <= 14, "a fill may reach 2^15 before it re-splits");
   int e = 0;
   bool have_scale = vmax > 0.0f && vmax <= 3.0e38f;
   if (have_scale) frexpf(vmax, &e);
-  float scale = ldexpf(1.0f, -e);
+  float scale = ldexpf(1.0f, kBS - e);
   int fidx = 0;  // fills so far (parity selects the fill's max slot)
 
   const float2 *__restrict__ vsub = visibilities + g.time_offset * C * 4;
@@ -564,7 +574,7 @@ __device__ __forceinline__ void grid_mfma(
         if (!(fm > 0.0f && fm <= 3.0e38f)) break;  // all zero (or non-finite)
         int em;
         frexpf(fm, &em);
-        if (have_scale ? em <= e + 15 : em == e) {
+        if (have_scale ? em <= e + 15 - kBS : em == e) {
           have_scale = true;
           break;
         }
@@ -578,7 +588,7 @@ __device__ __forceinline__ void grid_mfma(
           for (int i = 0; i < PY; ++i) accy[i] *= r;
         }
         e = em;
-        scale = ldexpf(1.0f, -e);
+        scale = ldexpf(1.0f, kBS - e);
         have_scale = true;
         }
         // Pull the next fill's rows into L2 while this fill's MFMA loop
@@ -755,7 +765,7 @@ __device__ __forceinline__ void grid_mfma(
           const bool last =
               j0 + cq_per_fill >= nchq && q0 + quads_per_fill >= nquads;
           if (!last && (fidx + 1) % kFlushFills == 0) {
-            const float unsc = ldexpf(1.0f, e);
+            const float unsc = ldexpf(1.0f, e - kBS);
 #pragma unroll
             for (int i = 0; i < PT; ++i) flush_tile(accx[i], i, unsc);
             if constexpr (!kFused) {
@@ -771,7 +781,7 @@ __device__ __forceinline__ void grid_mfma(
       // the master back into the hi columns (lanes col < 8), rescaled to
       // the current 2^-e (exact); the epilogue sums hi + lo as before
       if (flushed && col < 8) {
-        const float sc = ldexpf(1.0f, -e);
+        const float sc = ldexpf(1.0f, kBS - e);
 #pragma unroll
         for (int i = 0; i < PT; ++i) {
           const float4 m = *master(i);
@@ -787,7 +797,7 @@ __device__ __forceinline__ void grid_mfma(
       }
     }
 
-    const float unscale = ldexpf(1.0f, e);
+    const float unscale = ldexpf(1.0f, e - kBS);
     // ---- epilogue: X, Y tiles -> LDS [pixel][16]; base = X + Y, mirror =
     // X - Y; hi + lo; A-term; store ----
     __syncthreads();
