@@ -134,7 +134,7 @@ __device__ __forceinline__ void rotate_entry(float4 &pa, float4 &pb, float c,
 // instructions, half an MFMA.
 // ---------------------------------------------------------------------------
 #ifndef IDG_DEGRID_BSCALE
-#define IDG_DEGRID_BSCALE 0
+#define IDG_DEGRID_BSCALE 13
 #endif
 
 template <int KP>

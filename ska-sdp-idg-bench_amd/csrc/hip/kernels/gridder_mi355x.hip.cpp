@@ -61,7 +61,7 @@
 // the B operand's (visibilities') power-of-two scale targets a first-fill
 // maximum in [2^(kBS-1), 2^kBS)
 #ifndef IDG_GRID_BSCALE
-#define IDG_GRID_BSCALE 0
+#define IDG_GRID_BSCALE 12
 #endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW

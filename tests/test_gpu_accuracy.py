@@ -215,7 +215,8 @@ def test_c_defaults_closer_to_exact_than_the_reference(idg, oracle_lib,
     if direction == "gridder":
         assert split["ours_vs_exact"] <= split["ref_vs_exact"], fmt(split)
     else:
-        # the degridder is ~1.0e-6 from exact against the reference's
-        # 4.1e-7: bounded here at 5x the reference's own
-        # error, 10x under the bar
-        assert split["ours_vs_exact"] <= 5 * split["ref_vs_exact"], fmt(split)
+        # the degridder: 3.9e-7 against the reference's 4.1e-7 since its
+        # B operand sits high in the f16 range (1.0e-6 with
+        # the lo parts of small pixels in f16 subnormals): held to 1.25x
+        assert split["ours_vs_exact"] <= 1.25 * split["ref_vs_exact"], \
+            fmt(split)
