@@ -168,7 +168,6 @@ constexpr int kAddPix = kTW * kTH / 256;  // tile pixels per thread
 constexpr int kAddMaxTable = 256;  // shift phasors kept in LDS for S <= 128
 constexpr int kAddListCap = 1536;  // candidate entries sorted in LDS
 constexpr int kAddMaxRows = 64;    // home-tile rows a tile gathers from
-constexpr int kNoKey = 0x7fffffff;  // a candidate outside the tile
 constexpr int kSortLdsKeys = 19 * 1024;  // LDS: 2 x 76 KB (place kernel)
 constexpr int kSortMaxChunks = 16;       // workgroups of the LDS sort
 static_assert(kTW * kTH == 256 * kAddPix && (kTW & (kTW - 1)) == 0,
@@ -523,38 +522,40 @@ __global__ void __launch_bounds__(256)
   };
 
   __syncthreads();
-  const int n = nrows <= kAddMaxRows ? row_pre[nrows] : kAddListCap + 1;
-  if (n <= kAddListCap) {
-    // stage the candidates (key: the id when the subgrid overlaps the
-    // tile, else kNoKey), then sort the overlapping ones ascending by rank
-    // (subgrid indices are distinct): each entry's rank = the entries below
-    // it
+  // Compact the candidates that overlap the tile into the staging list (in
+  // any order: LDS atomic slots), so the list's cap bounds the overlapping
+  // subgrids, not every subgrid homed in the candidate rows; then sort them
+  // ascending by rank (subgrid indices are distinct: each entry's rank =
+  // the entries below it).  More overlaps than the cap take the ordered
+  // scan below.
+  if (tid == 0) wave_count[0] = 0;
+  __syncthreads();
+  if (nrows <= kAddMaxRows) {
+    const int n = row_pre[nrows];
     for (int i = tid; i < n; i += 256) {
       int r = 0;
       while (row_pre[r + 1] <= i) ++r;
       const int4 e = order[row_begin[r] + i - row_pre[r]];  // {s, x, y, z}
-      const int cx = e.y, cy = e.z;
-      cand_key[i] = overlaps(cx, cy) ? e.x : kNoKey;
-      cand_corner[i] = pack_corner(cx, cy);
+      if (!overlaps(e.y, e.z)) continue;
+      const int slot = atomicAdd(&wave_count[0], 1);
+      if (slot < kAddListCap) {
+        cand_key[slot] = e.x;
+        cand_corner[slot] = pack_corner(e.y, e.z);
+      }
     }
-    __syncthreads();
-    int mine = 0;
-    for (int i = tid; i < n; i += 256) {
+  }
+  __syncthreads();
+  const int m = nrows <= kAddMaxRows ? wave_count[0] : kAddListCap + 1;
+  if (m <= kAddListCap) {
+    for (int i = tid; i < m; i += 256) {
       const int k = cand_key[i];
-      if (k == kNoKey) continue;
       int rank = 0;
-      for (int j = 0; j < n; ++j) rank += cand_key[j] < k;
+      for (int j = 0; j < m; ++j) rank += cand_key[j] < k;
       keys[rank] = k;
       corner[rank] = cand_corner[i];
-      ++mine;
     }
-    // the overlapping count
-    int cnt = mine;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
-    if (lane == 0) wave_count[wave] = cnt;
     __syncthreads();
-    add_list(wave_count[0] + wave_count[1] + wave_count[2] + wave_count[3]);
+    add_list(m);
   } else {
     // ordered scan of all the metadata, 256 subgrids at a time
     for (int base = 0; base < nr_subgrids; base += 256) {

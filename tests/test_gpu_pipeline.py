@@ -68,8 +68,8 @@ def test_adder_matches_numpy(idg, S, G, W):
 
 
 def test_adder_crowded_tile_takes_ordered_scan(idg):
-    """More candidate subgrids for one grid tile than the adder's LDS list
-    holds (2048): that tile falls back to an ordered scan of the metadata; the result
+    """More subgrids overlapping one grid tile than the adder's LDS list
+    holds (1,536): that tile falls back to an ordered scan of the metadata; the result
     still matches numpy and is bit-reproducible."""
     import torch
     rng = np.random.default_rng(11)
@@ -78,6 +78,39 @@ def test_adder_crowded_tile_takes_ordered_scan(idg):
     md["x"] = rng.integers(0, 17, ns)        # all on tiles (0..1, 0..1)
     md["y"] = rng.integers(0, 17, ns)
     sub = rng.normal(size=(ns, 4, S, S)) + 1j * rng.normal(size=(ns, 4, S, S))
+    t_sub = torch.from_numpy(pl.to_pairs(sub)).cuda()
+    grids = []
+    for _ in range(2):
+        grid = torch.zeros((W, 4, G, G, 2), dtype=torch.float32, device="cuda")
+        idg.adder_launch(G, _md_tensor(md), t_sub, grid, W)
+        grids.append(grid)
+    torch.cuda.synchronize()
+    assert torch.equal(grids[0], grids[1])
+    ref = pl.adder(np.zeros((W, 4, G, G), complex), md,
+                   pl.to_complex(pl.to_pairs(sub)))
+    assert _rel(pl.to_complex(grids[0].cpu().numpy()), ref) < 1e-5
+
+
+def test_adder_many_homed_few_overlapping_keeps_the_list(idg):
+    """A tile whose candidate home-tile rows hold more subgrids than the
+    adder's LDS list (1,536) while only a few of them overlap the tile: the
+    list caps the overlapping subgrids (round 4; it used to cap every homed
+    candidate and send such a tile to the ordered scan).  2,000 subgrids
+    homed two tiles left of tile (2, 0) and ending before it, 60 overlapping
+    it: the grid matches numpy and is bit-reproducible."""
+    import torch
+    rng = np.random.default_rng(13)
+    S, G, W = 32, 128, 1
+    n_far, n_near = 2000, 60
+    md = np.zeros(n_far + n_near, METADATA_DTYPE)
+    md["x"][:n_far] = 0                      # home tile 0, covers x < 32
+    md["y"][:n_far] = rng.integers(0, 8, n_far)
+    md["x"][n_far:] = rng.integers(17, 40, n_near)   # overlaps x in [32, 48)
+    md["y"][n_far:] = rng.integers(0, 8, n_near)
+    order = rng.permutation(md.size)         # homed ones spread over ids
+    md = md[order]
+    sub = rng.normal(size=(md.size, 4, S, S)) + \
+        1j * rng.normal(size=(md.size, 4, S, S))
     t_sub = torch.from_numpy(pl.to_pairs(sub)).cuda()
     grids = []
     for _ in range(2):
