@@ -31,11 +31,11 @@ import oracle as orc  # noqa: E402
 from mfma_accum_emul import IH, IH_LO, TAIL, f32, f64, fma32  # noqa: E402
 
 
-def main():
-    C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    T = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+def emulate(C, T, nthreads=8):
+    """{model: distance to the exact sum in the reference metric} for the
+    two subgrids of the -c geometry at C channels and T timesteps."""
     S, G = 32, 1024
-    a = idg_amd.generate(2, 2, T, C, G, S, nthreads=8)
+    a = idg_amd.generate(2, 2, T, C, G, S, nthreads=nthreads)
     ns = a["metadata"].size
     img = f32(idg_amd.IMAGE_SIZE)
     k = a["wavenumbers"].astype(f32)
@@ -98,10 +98,17 @@ def main():
             outs[x][s, ..., 0] = Q.real.T.reshape(4, S, S)
             outs[x][s, ..., 1] = Q.imag.T.reshape(4, S, S)
     o = orc.Oracle()
-    print(f"C={C} T={T}, {ns} subgrids: emulated reduction vs exact "
+    return {x: float(o.check_error(outs[x], outs["exact"])[0]) for x in models}
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    T = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+    errs = emulate(C, T)
+    print(f"C={C} T={T}, 2 subgrids: emulated reduction vs exact "
           "(double sums), reference metric")
-    for x in models:
-        print(f"  {x:6s} {o.check_error(outs[x], outs['exact'])[0]:.3e}")
+    for x, e in errs.items():
+        print(f"  {x:7s} {e:.3e}")
 
 
 if __name__ == "__main__":

@@ -205,3 +205,21 @@ def test_reference_itself_misses_the_bar_at_large_TxC(oracle_lib):
         errs[C] = oracle_lib.check_error(r, e.astype(np.float32))[0]
     assert errs[16] < 2e-6, errs
     assert errs[256] > TOLERANCE, errs
+
+
+@pytest.mark.parametrize("C", [16, 64])
+def test_reduction_tail_on_one_channel_per_quad_emulated(C):
+    """The gridder's phase-reduction tail, emulated exactly with double sums
+    (tests/debug/tail_mean_emul.py): without it the
+    coherent sums keep a systematic phase error; added as 4c to the first
+    channel of every quad (kPrecTailAlt, the shipped gridder) it is as close
+    to the exact sum as the every-phasor add within 2x, and at least 4x
+    closer than none -- while a per-quad pattern or one channel in 16 is
+    worse than one in 4."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "debug"))
+    from tail_mean_emul import emulate
+    e = emulate(C, 128, nthreads=4)
+    assert e["alt4"] <= 2.0 * e["block"], e
+    assert e["alt4"] * 4.0 <= e["none"], e
+    assert e["alt4"] < e["sparse4"] and e["alt4"] < e["alt16"], e
