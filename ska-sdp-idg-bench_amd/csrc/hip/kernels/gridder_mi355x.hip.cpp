@@ -302,7 +302,9 @@ __device__ __forceinline__ void l2_prefetch_dma(const void *src,
 // (kernel_subgrid_fft_reg's) runs on them (idg_gridder_fft_launch).
 // PREC: kPrecTail adds the k * phase_index part of the reduction's tail to
 // every phasor's revolutions (device.hpp tail_k_rev: one v_pk_add_f32 per
-// two phasors, ~5 % of the MFMA loop); kPrecFlush (S = 32) adds the
+// two phasors, ~5 % of the MFMA loop); kPrecTailAlt adds 4x that to the
+// first channel of every quad only (the default: the same sum over each
+// quad for a quarter of the adds); kPrecFlush (S = 32) adds the
 // accumulator tiles to an f32 master every kFlushFills fills and restarts
 // them from zero (blocked summation, DESIGN.md §3.1: the MFMA rounds its
 // f32 sum several times per instruction, so 2,048 K-steps into one tile put
