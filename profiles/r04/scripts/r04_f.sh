@@ -13,4 +13,4 @@ for l in bs0 bs13; do
 done
 cat $out/accuracy.jsonl | cut -c1-220
 bash tests/debug/session.sh $out/ab ab=ab/bs0.so,ab/bs13.so 'suite@ab/bs13.so=gridder or degridder' || exit 1
-bash tests/debug/r04_wl_s64.sh
+bash profiles/r04/scripts/r04_wl_s64.sh

@@ -8,5 +8,5 @@ cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r04g
 mkdir -p $out
 bash tests/debug/session.sh $out/s suite smoke  # a failing test does not end the call
-bash tests/debug/r04_wl_s64.sh || exit 1
+bash profiles/r04/scripts/r04_wl_s64.sh || exit 1
 bash tests/debug/session.sh $out/c profile=r04c256f8,--workload,c256
