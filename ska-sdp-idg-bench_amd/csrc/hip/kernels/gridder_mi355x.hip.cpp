@@ -507,7 +507,13 @@ __device__ __forceinline__ void grid_mfma(
           const unsigned off_s = (grp * C * 8 + w_s) * 4u;
           int qq = wv / nj, jj = wv - (wv / nj) * nj;
           float lmax = 0.0f;  // max |raw value| this lane loads
+#ifdef IDG_DEBUG_SKIPFILL
+          // timing experiment only (wrong output): every fill after the
+          // first reuses its B fragments
+          for (int ks = fidx > 0 ? nks : wv; ks < nks; ks += NW) {
+#else
           for (int ks = wv; ks < nks; ks += NW) {
+#endif
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
             float bc[4], bs[4];
