@@ -242,19 +242,8 @@ __device__ __forceinline__ void pixel_geometry(int p, int S, float image_size,
 // (x, x, y, y) per lane, stored pre-expanded in LDS.  Per phasor: 1 packed
 // phase instruction, v_sin + v_cos, 3 split instructions, half an MFMA.
 // ---------------------------------------------------------------------------
-// IDG_GRID_STAGE: each fill's raw visibility rows are copied into LDS by
-// LDS-DMA during the previous fill's MFMA loop, so the fill reads LDS, not
-// L2 (24 K-steps per fill: the 48 KB of B fragments and the 12 KB staging
-// buffer share the epilogue's 64 KB)
-#ifndef IDG_GRID_STAGE
-#define IDG_GRID_STAGE 0
-#endif
 #ifndef IDG_GRID_KSBUF
-#if IDG_GRID_STAGE
-#define IDG_GRID_KSBUF 24
-#else
 #define IDG_GRID_KSBUF 32
-#endif
 #endif
 constexpr int kKsBuf = IDG_GRID_KSBUF;  // K-steps (16 items each) of B fragments per fill
 
@@ -265,14 +254,9 @@ template <int AT, int NW>
 struct MfmaLds {
   static constexpr int kObufFloats = NW * 16 * AT * 16;  // accumulator tiles
   static constexpr int kBbufWords = kKsBuf * 64 * 8;  // uint4 X + uint4 Y
-  // raw rows of the next fill (IDG_GRID_STAGE): 512 B per K-step, after the
-  // B fragments, inside the epilogue's accumulator region
-  static constexpr int kStageOff = kBbufWords;
-  static constexpr int kStageWords = IDG_GRID_STAGE ? kKsBuf * 128 : 0;
   // uvw of the fill's timesteps (at most 4 * kKsBuf), float4 each
-  static constexpr int kUvwOff = kObufFloats > kBbufWords + kStageWords
-                                     ? kObufFloats
-                                     : kBbufWords + kStageWords;
+  static constexpr int kUvwOff =
+      kObufFloats > kBbufWords ? kObufFloats : kBbufWords;
   static constexpr int kRedOff = kUvwOff + 4 * 4 * kKsBuf;  // 8 floats
   static constexpr int kSlotOff = kRedOff + 8;   // 2 fill maxima (bits)
   static constexpr int kSinkOff = kSlotOff + 2;  // 64 words: prefetch sink
@@ -298,25 +282,6 @@ constexpr int general_lds_words() {
 // SALU write of M0 is followed by one wait state before the LDS-DMA reads
 // it (the gfx9 "M0 write -> LDS DMA" hazard, which the compiler cannot pad
 // inside an asm string; tests/probes/dma_drain_check.py checks the listing).
-// LDS-DMA of 16 bytes per lane from the lane's global address into
-// lds_dst + 16 * lane (lds_dst wave-uniform): the staged fill's copy of the
-// next fill's raw rows (IDG_GRID_STAGE).  The same M0 handling as
-// l2_prefetch_dma below; hipcc counts no wait for it, so the fill that reads
-// the copy first waits for vmcnt(0) itself, then the barrier.
-__device__ __forceinline__ void stage_dma16(const void *src,
-                                            const void *lds_dst) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(
-      reinterpret_cast<size_t>((const __attribute__((address_space(3))) void *)
-                                   lds_dst)));
-  unsigned saved;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(saved)
-      : "v"(src), "s"(m0)
-      : "memory");
-}
-
 __device__ __forceinline__ void l2_prefetch_dma(const void *src,
                                                 const void *lds_dst) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(
@@ -504,16 +469,10 @@ __device__ __forceinline__ void grid_mfma(
       a = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
     };
 
-    // this fill's raw rows are in the LDS staging buffer (IDG_GRID_STAGE)
-    bool staged = false;
     for (int q0 = 0; q0 < nquads; q0 += quads_per_fill) {
       const int nq = min(quads_per_fill, nquads - q0);
       for (int j0 = 0; j0 < nchq; j0 += cq_per_fill, ++fidx) {
         const int nj = min(cq_per_fill, nchq - j0);
-        // the wave's own LDS-DMA into the staging buffer has landed (the
-        // barrier below then makes every wave's copy visible)
-        if (IDG_GRID_STAGE && staged)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // ---- B fragments for nq timestep quads x nj channel quads -> LDS.
         // One wave fills one K-step (lane = group g, column col): items
         // (t = 4q+g, c0..c0+3), two word loads each, scaled, then split to
@@ -558,20 +517,7 @@ __device__ __forceinline__ void grid_mfma(
             const int t = (q0 + qq) * 4 + grp;
             const int c0 = 4 * (j0 + jj);
             float bc[4], bs[4];
-            if (IDG_GRID_STAGE && staged) {
-              // row qq * 4 + grp of the fill, channel quad jj: 128 B
-              const float *stg = reinterpret_cast<const float *>(
-                                     lds + Lds::kStageOff) +
-                                 ((qq * 4 + grp) * nj + jj) * 32;
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const float rc = stg[u * 8 + w_c];
-                const float rs = stg[u * 8 + w_s];
-                lmax = fmaxf(lmax, fmaxf(fabsf(rc), fabsf(rs)));
-                bc[u] = rc * scale;
-                bs[u] = rs * sc_s;
-              }
-            } else if (full) {
+            if (full) {
               const char *blk = reinterpret_cast<const char *>(
                   vsubf + ((q0 + qq) * 4 * C + c0) * 8);
 #pragma unroll
@@ -661,30 +607,7 @@ __device__ __forceinline__ void grid_mfma(
             j0n = 0;
             q0n = q0 + quads_per_fill;
           }
-          const int nqn = min(quads_per_fill, nquads - q0n);
-          const int njn = min(cq_per_fill, nchq - j0n);
-          const bool next_full =
-              q0n < nquads && (q0n + nqn) * 4 <= nt && 4 * (j0n + njn) <= C;
-          staged = IDG_GRID_STAGE && next_full;
-          if (IDG_GRID_STAGE && next_full) {
-            // the next fill's rows (4 nqn of them, channel quads j0n ..
-            // j0n + njn: 128 B each) into the staging buffer, 16 B per lane
-            // and 1 KB per wave-instruction; its reads wait for them
-            const char *vb = reinterpret_cast<const char *>(vsub);
-            const int per_row = njn * 8;  // 16-byte chunks per row
-            const int total = 4 * nqn * per_row;
-            const int wv = __builtin_amdgcn_readfirstlane(wave);
-            for (int cb = wv * 64; cb < total; cb += NW * 64) {
-              const int i = cb + lane;
-              if (i < total) {
-                const int r = i / per_row, rem = i - (i / per_row) * per_row;
-                stage_dma16(vb + (static_cast<size_t>(4 * q0n + r) * C +
-                                  4 * j0n) * 32 + rem * 16,
-                            reinterpret_cast<const char *>(
-                                lds + Lds::kStageOff) + cb * 16);
-              }
-            }
-          } else if (q0n < nquads) {
+          if (q0n < nquads) {
             const int rows = min(4 * (q0n + quads_per_fill), nt) - 4 * q0n;
             const int lpr = (min(cq_per_fill, nchq - j0n) * 128 + 127) / 128;
             const char *vb = reinterpret_cast<const char *>(vsub);
