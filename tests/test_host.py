@@ -160,6 +160,20 @@ def test_kernel_selection_names():
     assert idg_amd.kernel_name("gridder", 33, 3) == "gridder_mi355x_generic"
 
 
+def test_precision_options_defaults_and_override(monkeypatch):
+    # util.cpp precision_for: gridder tail on one channel per quad, blocked
+    # summation above 16 channels; degridder neither; IDG_PREC overrides
+    monkeypatch.delenv("IDG_PREC", raising=False)
+    assert idg_amd.precision_options("gridder", 32, 16) == (
+        4, "reduction tail on one channel per quad")
+    bits, desc = idg_amd.precision_options("gridder", 32, 256)
+    assert bits == 6 and "blocked summation" in desc
+    assert idg_amd.precision_options("degridder", 32, 256) == (0, "none")
+    monkeypatch.setenv("IDG_PREC", "1")
+    assert idg_amd.precision_options("gridder", 32, 16)[0] == 1
+    assert idg_amd.precision_options("degridder", 64, 16)[0] == 1
+
+
 def test_shard_plan_and_rebase():
     d = idg_amd.generate(6, 3, 8, 2, 512, 16, want=("metadata",))
     md = d["metadata"]
