@@ -312,14 +312,14 @@ __device__ __forceinline__ void l2_prefetch_dma(const void *src,
 // the subgrid's own output slot (32 KB at S = 32, one pass), which only the
 // epilogue writes, after the master is read back.
 template <int S_CT, int PT, int CB, int NW, bool MIRROR, bool FFT = false,
-          int PREC = kPrecTail>
+          int PREC = kPrecTail, bool PRESCAN = false>
 __device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
     const float *__restrict__ wavenumbers,
     const float2 *__restrict__ visibilities,
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
-    float2 *__restrict__ out, unsigned *lds) {
+    float2 *__restrict__ out, unsigned *lds, float vmax_pre = 0.0f) {
   static_assert(CB % 4 == 0, "anchor blocks hold whole channel quads");
   // General path: an opaque copy of the thread index, so values derived
   // from it are formed per call, not hoisted out of the general kernel's
@@ -365,9 +365,11 @@ __device__ __forceinline__ void grid_mfma(
   // yet set, is split again with the new scale after the f32 sums so far
   // are rescaled by the exact power of two.  Each input byte is thus read
   // once per fill (the first fill's rows twice, back to back, from L2).
-  float vmax = 0.0f;
-  {
-    if (tid < 2) slots[tid] = 0u;
+  // PRESCAN: the caller scanned them already (prologue_scan: vmax_pre).
+  float vmax = vmax_pre;
+  if (tid < 2) slots[tid] = 0u;
+  if constexpr (!PRESCAN) {
+    vmax = 0.0f;
     const float4 *v4 = reinterpret_cast<const float4 *>(
         visibilities + g.time_offset * C * 4);
     const int n4 = min(4 * quads_per_fill, nt) * C * 2;
@@ -908,6 +910,48 @@ __device__ __forceinline__ void grid_mfma(
   }
 }
 
+// The mirror check's uvw loads and grid_mfma's max-|V| scan of the first
+// fill's rows in one pass: both depend only on the subgrid's metadata, so
+// the prologue waits for one memory round trip and one barrier instead of
+// two of each (the first round of workgroups, all in their prologue at
+// once, has no other workgroup computing beside it).  Returns this thread's
+// w != 0 flag and leaves each wave's maximum in red[wave]; the caller's
+// __syncthreads_or is the barrier before prologue_max reads them.
+template <int NW>
+__device__ __forceinline__ bool prologue_scan(
+    const SubgridSetup &g, int C,
+    const idg::UVWCoordinate<float> *__restrict__ uvw,
+    const float2 *__restrict__ visibilities, float *red) {
+  const int tid = threadIdx.x;
+  bool w_nonzero = false;
+  for (int t = tid; t < g.nr_timesteps; t += NW * 64)
+    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+  // grid_mfma's first fill: quads_per_fill timestep quads, all channels
+  const int nchq = (C + 3) / 4;
+  const int quads_per_fill = nchq <= kKsBuf ? kKsBuf / nchq : 1;
+  const float4 *v4 = reinterpret_cast<const float4 *>(
+      visibilities + g.time_offset * C * 4);
+  const int n4 = min(4 * quads_per_fill, g.nr_timesteps) * C * 2;
+  float vmax = 0.0f;
+  for (int i = tid; i < n4; i += NW * 64) {
+    const float4 q = v4[i];
+    vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)),
+                             fmaxf(fabsf(q.z), fabsf(q.w))));
+  }
+  for (int off = 32; off > 0; off >>= 1)
+    vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+  if ((tid & 63) == 0) red[tid >> 6] = vmax;
+  return w_nonzero;
+}
+
+template <int NW>
+__device__ __forceinline__ float prologue_max(const float *red) {
+  float vmax = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) vmax = fmaxf(vmax, red[w]);
+  return vmax;
+}
+
 }  // namespace
 
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
@@ -950,12 +994,6 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 
   // Mirror pairs need w = 0 on every timestep of the subgrid (checked once,
   // so the two paths below stay separate loops with separate registers).
-  bool w_nonzero = false;
-  for (int t = tid; t < g.nr_timesteps; t += blockDim.x)
-    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-  const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
-                      g.w_offset == 0.0f;
-
   if constexpr (MODE == 1) {
     constexpr int NW = IDG_GRID_NW;
     // both paths hold 2 PT accumulator tiles per wave
@@ -963,20 +1001,32 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
     timeline_start(idg_debug_timeline_gridder);
 #endif
+    float *red = reinterpret_cast<float *>(lds + MfmaLds<2 * PT, NW>::kRedOff);
+    const bool mirror =
+        __syncthreads_or(prologue_scan<NW>(g, C, uvw, visibilities, red)) ==
+            0 &&
+        S % 2 == 0 && g.w_offset == 0.0f;
+    const float vmax = prologue_max<NW>(red);
     if (mirror)
-      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC>(
+      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
           g, S, npix, image_size, C, nr_stations, uvw, wavenumbers,
-          visibilities, spheroidal, aterms, out, lds);
+          visibilities, spheroidal, aterms, out, lds, vmax);
     else
       grid_mfma<S_CT, IDG_GRID_FUSED_GENERAL ? 2 * PT : PT, CB, NW, false,
-                FFT, PREC>(g, S, npix, image_size, C, nr_stations, uvw,
-                           wavenumbers, visibilities, spheroidal, aterms, out,
-                           lds);
+                FFT, PREC, true>(g, S, npix, image_size, C, nr_stations, uvw,
+                                 wavenumbers, visibilities, spheroidal, aterms,
+                                 out, lds, vmax);
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
     timeline_end(idg_debug_timeline_gridder);
 #endif
     return;
   }
+
+  bool w_nonzero = false;
+  for (int t = tid; t < g.nr_timesteps; t += blockDim.x)
+    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
+  const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
+                      g.w_offset == 0.0f;
 
   if (mirror) {
     // Mirror-pair path: lane owns base pixels b (< npix/2) and npix-1-b.
@@ -1083,19 +1133,20 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
   const int tid = threadIdx.x;
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);
-  bool w_nonzero = false;
-  for (int t = tid; t < g.nr_timesteps; t += blockDim.x)
-    w_nonzero |= uvw[g.time_offset + t].w != 0.0f;
-  const bool mirror = __syncthreads_or(w_nonzero) == 0 && S % 2 == 0 &&
-                      g.w_offset == 0.0f;
+  float *red = reinterpret_cast<float *>(lds + MfmaLds<2 * PT, NW>::kRedOff);
+  const bool mirror =
+      __syncthreads_or(prologue_scan<NW>(g, nr_channels, uvw, visibilities,
+                                         red)) == 0 &&
+      S % 2 == 0 && g.w_offset == 0.0f;
   if (!mirror) {
     if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
-  grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC>(
+  grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
-      subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+      subgrids + static_cast<size_t>(s) * 4 * npix, lds,
+      prologue_max<NW>(red));
 }
 
 template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
