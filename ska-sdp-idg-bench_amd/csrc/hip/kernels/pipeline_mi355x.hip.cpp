@@ -400,11 +400,72 @@ __global__ void __launch_bounds__(1024)
 // home sort's ranges and sorted in LDS; a candidate list larger than the
 // LDS list falls back to an ordered scan of all the metadata, which yields
 // the same order.
+//
+// Crowded tiles (round 4): one workgroup per tile serialises a crowded uv
+// centre onto a few CUs (24,500 subgrids around the centre: 0.2 -> 6.6 ms,
+// DESIGN.md §11).  A tile whose ordered list holds more than kAddSegLen
+// entries is cut into segments of kAddSegLen: its own workgroup sums the
+// first into a partial tile, kAddWorkers workgroups launched after the
+// tiles sum the others (taking the partial slots from a counter), and the
+// workgroup that finishes a tile's last segment adds the partials to the
+// grid in segment order.  Deterministic (a segment's sum and the order of
+// the partials depend on the data only); a tile with at most kAddSegLen
+// entries takes the single-workgroup path unchanged, bit for bit.
+constexpr int kAddSegLen = 256;   // list entries per segment
+constexpr int kAddWorkers = 256;  // segment workgroups after the tiles
+// counters, each on its own 128-byte line; zero between launches
+constexpr int kSegHeavy = 0, kSegTotal = 32, kSegTake = 64, kSegMainDone = 96,
+              kSegExit = 128, kSegHdrInts = 160;
+constexpr size_t kAddPartialFloat2 = static_cast<size_t>(kAddPix) * 4 * 256;
+
+// The segment workspace (util.hpp WorkspaceLease, cached per stream):
+// counters | partial [slot][pixel j][pol][thread] | heavy {tile, z, nseg,
+// base} | done (segments finished per crowded tile) | owner (crowded tile
+// of each partial slot).  Sized for the worst case of the batch, so that
+// no tile is ever refused (which tiles split must not depend on the order
+// of the atomics): a subgrid overlaps at most tps tiles, so the lists hold
+// at most T = nr_subgrids * tps entries, at most T / kAddSegLen tiles are
+// crowded, and their segments number at most 2 T / kAddSegLen.
+struct AdderSeg {
+  int *hdr = nullptr;
+  float2 *partial = nullptr;
+  int4 *heavy = nullptr;
+  int *done = nullptr;
+  int *owner = nullptr;
+  int heavy_cap = 0, slot_cap = 0;
+};
+
+struct AdderSegCaps {
+  int heavy, slots;
+  size_t bytes;
+};
+inline AdderSegCaps adder_seg_caps(int nr_subgrids, int S, int ntiles_all) {
+  const long long cols_x = (S - 1 + kTW - 1) / kTW + 1;
+  const long long cols_y = (S - 1 + kTH - 1) / kTH + 1;
+  const long long entries = static_cast<long long>(nr_subgrids) * cols_x * cols_y;
+  const long long per = (entries + kAddSegLen - 1) / kAddSegLen;
+  AdderSegCaps c;
+  c.heavy = static_cast<int>(std::min<long long>(ntiles_all, per + 1));
+  c.slots = static_cast<int>(2 * per + 1);
+  c.bytes = kSegHdrInts * sizeof(int) +
+            static_cast<size_t>(c.slots) *
+                (kAddPartialFloat2 * sizeof(float2) + sizeof(int)) +
+            static_cast<size_t>(c.heavy) * (sizeof(int4) + sizeof(int));
+  return c;
+}
+
+// relaxed device-scope loads of what other workgroups of the launch wrote
+// (after the acquire fence that follows their counter)
+__device__ __forceinline__ int load_agent(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(256)
     kernel_adder(const idg::Metadata *__restrict__ metadata, int nr_subgrids,
                  const int *__restrict__ offset, const int4 *__restrict__ order,
                  const float2 *__restrict__ subgrids,
-                 float2 *__restrict__ grid, int G, int S, int nr_w_layers) {
+                 float2 *__restrict__ grid, int G, int S, int nr_w_layers,
+                 AdderSeg sw, int nworkers) {
   // the list (subgrid ids ascending, their corners relative to the tile
   // packed as (y - ty0 + S) << 16 | (x - tx0 + S), both in (0, S + T)) and
   // the candidates staged for it
@@ -412,15 +473,11 @@ __global__ void __launch_bounds__(256)
   __shared__ int cand_key[kAddListCap], cand_corner[kAddListCap];
   __shared__ int row_begin[kAddMaxRows], row_pre[kAddMaxRows + 1];
   __shared__ int wave_count[4];
+  __shared__ int bcast[4];
   __shared__ float2 table[kAddMaxTable];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TileGrid tg(G);
-  // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal neighbours,
-  // whose subgrid reads share cache lines, run on the same XCD's L2
-  const int tl = xcd_subgrid(blockIdx.x, gridDim.x);
-  const int tx = tl % tg.ntx, ty = tl / tg.ntx;
-  const int tx0 = tx * kTW, ty0 = ty * kTH;
-  const int z = blockIdx.y;
+  const int ntiles = tg.ntx * tg.nty;
   const int npix = S * S;
   const bool tabled = 2 * S - 1 <= kAddMaxTable;
   // shift phasor depends on x + y only
@@ -428,180 +485,326 @@ __global__ void __launch_bounds__(256)
     for (int k = tid; k < 2 * S - 1; k += 256)
       table[k] = unit_phasor(k * (S + 1) - S, 2 * S, 1.0f);
 
-  // candidates: home tiles (tx - dx, ty - dy), dx <= DX, dy <= DY, one
-  // contiguous range of order[] per home-tile row
-  const int DX = (S - 1 + kTW - 1) / kTW, DY = (S - 1 + kTH - 1) / kTH;
-  const int nrows = min(DY, ty) + 1;
-  const int hx0 = max(0, tx - DX);
-  if (wave == 0 && nrows <= kAddMaxRows) {
-    int len = 0;
-    if (lane < nrows) {
-      const int k0 = (z * tg.nty + ty - lane) * tg.ntx;
-      const int b = offset[k0 + hx0];
-      len = offset[k0 + tx + 1] - b;
-      row_begin[lane] = b;
-    }
-    int incl = len;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int o = __shfl_up(incl, d);
-      if (lane >= d) incl += o;
-    }
-    if (lane < nrows) row_pre[lane + 1] = incl;
-    if (lane == 0) row_pre[0] = 0;
-  }
+  // Tile tl of layer z.  seg < 0: the tile's own workgroup (the whole list,
+  // or its first segment when crowded); seg >= 1: that segment of crowded
+  // tile h (heavy entry he).
+  auto add_tile = [&](int tl, int z, int seg, int h, int4 he) {
+    const int tx = tl % tg.ntx, ty = tl / tg.ntx;
+    const int tx0 = tx * kTW, ty0 = ty * kTH;
 
-  float2 acc[kAddPix][4];
+    // candidates: home tiles (tx - dx, ty - dy), dx <= DX, dy <= DY, one
+    // contiguous range of order[] per home-tile row
+    const int DX = (S - 1 + kTW - 1) / kTW, DY = (S - 1 + kTH - 1) / kTH;
+    const int nrows = min(DY, ty) + 1;
+    const int hx0 = max(0, tx - DX);
+    __syncthreads();  // the previous tile's LDS is consumed
+    if (wave == 0 && nrows <= kAddMaxRows) {
+      int len = 0;
+      if (lane < nrows) {
+        const int k0 = (z * tg.nty + ty - lane) * tg.ntx;
+        const int b = offset[k0 + hx0];
+        len = offset[k0 + tx + 1] - b;
+        row_begin[lane] = b;
+      }
+      int incl = len;
 #pragma unroll
-  for (int j = 0; j < kAddPix; ++j)
-#pragma unroll
-    for (int pol = 0; pol < 4; ++pol) acc[j][pol] = make_float2(0.0f, 0.0f);
+      for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+      }
+      if (lane < nrows) row_pre[lane + 1] = incl;
+      if (lane == 0) row_pre[0] = 0;
+    }
 
-  // add the entries [0, total) of the LDS list, in list order; U entries
-  // per step with every load issued before the first add (lanes outside an
-  // entry's subgrid load its pixel 0 and drop it)
-  constexpr int U = IDG_ADD_U;
-  auto add_list = [&](int total) {
-    for (int e = 0; e < total; e += U) {
-      float2 v[U][kAddPix][4];
-      float2 ph[U][kAddPix];
-      bool ok[U][kAddPix];
+    float2 acc[kAddPix][4];
 #pragma unroll
-      for (int h = 0; h < U; ++h) {
-        const int ee = min(e + h, total - 1);
-        const int2 c = make_int2(tx0 - S + (corner[ee] & 0xffff),
-                                 ty0 - S + (corner[ee] >> 16));
-        const float2 *sg =
-            subgrids + static_cast<size_t>(keys[ee]) * 4 * npix;
+    for (int j = 0; j < kAddPix; ++j)
 #pragma unroll
-        for (int j = 0; j < kAddPix; ++j) {
-          const int i = tid + 256 * j;
-          const int x = tx0 + (i & (kTW - 1)) - c.x;
-          const int y = ty0 + i / kTW - c.y;
-          ok[h][j] = e + h < total && x >= 0 && x < S && y >= 0 && y < S;
-          const int src =
-              ok[h][j] ? half_shift(y, S) * S + half_shift(x, S) : 0;
-          ph[h][j] = !ok[h][j] ? make_float2(0.0f, 0.0f)
-                     : tabled  ? table[x + y]
-                               : shift_phasor(x, y, S, 1.0f);
+      for (int pol = 0; pol < 4; ++pol) acc[j][pol] = make_float2(0.0f, 0.0f);
+
+    // add the entries [e0, e1) of the LDS list, in list order; U entries
+    // per step with every load issued before the first add (lanes outside
+    // an entry's subgrid load its pixel 0 and drop it)
+    constexpr int U = IDG_ADD_U;
+    auto add_list = [&](int e0, int e1) {
+      for (int e = e0; e < e1; e += U) {
+        float2 v[U][kAddPix][4];
+        float2 ph[U][kAddPix];
+        bool ok[U][kAddPix];
+#pragma unroll
+        for (int hh = 0; hh < U; ++hh) {
+          const int ee = min(e + hh, e1 - 1);
+          const int2 c = make_int2(tx0 - S + (corner[ee] & 0xffff),
+                                   ty0 - S + (corner[ee] >> 16));
+          const float2 *sg =
+              subgrids + static_cast<size_t>(keys[ee]) * 4 * npix;
+#pragma unroll
+          for (int j = 0; j < kAddPix; ++j) {
+            const int i = tid + 256 * j;
+            const int x = tx0 + (i & (kTW - 1)) - c.x;
+            const int y = ty0 + i / kTW - c.y;
+            ok[hh][j] = e + hh < e1 && x >= 0 && x < S && y >= 0 && y < S;
+            const int src =
+                ok[hh][j] ? half_shift(y, S) * S + half_shift(x, S) : 0;
+            ph[hh][j] = !ok[hh][j] ? make_float2(0.0f, 0.0f)
+                        : tabled   ? table[x + y]
+                                   : shift_phasor(x, y, S, 1.0f);
 #if IDG_ADD_MASKED
-          // lanes outside the entry's subgrid issue no load (a wave with
-          // none inside skips the entry's loads)
-          if (ok[h][j]) {
+            // lanes outside the entry's subgrid issue no load (a wave with
+            // none inside skips the entry's loads)
+            if (ok[hh][j]) {
 #pragma unroll
-            for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = sg[pol * npix + src];
-          } else {
+              for (int pol = 0; pol < 4; ++pol)
+                v[hh][j][pol] = sg[pol * npix + src];
+            } else {
 #pragma unroll
-            for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = make_float2(0.f, 0.f);
-          }
+              for (int pol = 0; pol < 4; ++pol)
+                v[hh][j][pol] = make_float2(0.f, 0.f);
+            }
 #else
 #pragma unroll
-          for (int pol = 0; pol < 4; ++pol) v[h][j][pol] = sg[pol * npix + src];
+            for (int pol = 0; pol < 4; ++pol)
+              v[hh][j][pol] = sg[pol * npix + src];
 #endif
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < U; ++h)
-#pragma unroll
-        for (int j = 0; j < kAddPix; ++j) {
-          if (!ok[h][j]) continue;
-#pragma unroll
-          for (int pol = 0; pol < 4; ++pol) {
-            const float2 w = cmulf(ph[h][j], v[h][j][pol]);
-            acc[j][pol].x += w.x;
-            acc[j][pol].y += w.y;
           }
         }
-    }
-  };
-  auto pack_corner = [&](int cx, int cy) {
-    return (cy - ty0 + S) << 16 | (cx - tx0 + S);
-  };
-  auto overlaps = [&](int cx, int cy) {
-    return cx < tx0 + kTW && cx + S > tx0 && cy < ty0 + kTH && cy + S > ty0;
-  };
-
-  __syncthreads();
-  // Compact the candidates that overlap the tile into the staging list (in
-  // any order: LDS atomic slots), so the list's cap bounds the overlapping
-  // subgrids, not every subgrid homed in the candidate rows; then sort them
-  // ascending by rank (subgrid indices are distinct: each entry's rank =
-  // the entries below it).  More overlaps than the cap take the ordered
-  // scan below.
-  if (tid == 0) wave_count[0] = 0;
-  __syncthreads();
-  if (nrows <= kAddMaxRows) {
-    const int n = row_pre[nrows];
-    for (int i = tid; i < n; i += 256) {
-      int r = 0;
-      while (row_pre[r + 1] <= i) ++r;
-      const int4 e = order[row_begin[r] + i - row_pre[r]];  // {s, x, y, z}
-      if (!overlaps(e.y, e.z)) continue;
-      const int slot = atomicAdd(&wave_count[0], 1);
-      if (slot < kAddListCap) {
-        cand_key[slot] = e.x;
-        cand_corner[slot] = pack_corner(e.y, e.z);
+#pragma unroll
+        for (int hh = 0; hh < U; ++hh)
+#pragma unroll
+          for (int j = 0; j < kAddPix; ++j) {
+            if (!ok[hh][j]) continue;
+#pragma unroll
+            for (int pol = 0; pol < 4; ++pol) {
+              const float2 w = cmulf(ph[hh][j], v[hh][j][pol]);
+              acc[j][pol].x += w.x;
+              acc[j][pol].y += w.y;
+            }
+          }
       }
-    }
-  }
-  __syncthreads();
-  const int m = nrows <= kAddMaxRows ? wave_count[0] : kAddListCap + 1;
-  if (m <= kAddListCap) {
-    for (int i = tid; i < m; i += 256) {
-      const int k = cand_key[i];
-      int rank = 0;
-      for (int j = 0; j < m; ++j) rank += cand_key[j] < k;
-      keys[rank] = k;
-      corner[rank] = cand_corner[i];
+    };
+    auto pack_corner = [&](int cx, int cy) {
+      return (cy - ty0 + S) << 16 | (cx - tx0 + S);
+    };
+    auto overlaps = [&](int cx, int cy) {
+      return cx < tx0 + kTW && cx + S > tx0 && cy < ty0 + kTH && cy + S > ty0;
+    };
+
+    __syncthreads();
+    // Compact the candidates that overlap the tile into the staging list
+    // (in any order: LDS atomic slots), so the list's cap bounds the
+    // overlapping subgrids, not every subgrid homed in the candidate rows;
+    // then sort them ascending by rank (subgrid indices are distinct: each
+    // entry's rank = the entries below it).  More overlaps than the cap
+    // take the ordered scan below.  The count is exact either way.
+    if (tid == 0) wave_count[0] = 0;
+    __syncthreads();
+    if (nrows <= kAddMaxRows) {
+      const int n = row_pre[nrows];
+      for (int i = tid; i < n; i += 256) {
+        int r = 0;
+        while (row_pre[r + 1] <= i) ++r;
+        const int4 e = order[row_begin[r] + i - row_pre[r]];  // {s, x, y, z}
+        if (!overlaps(e.y, e.z)) continue;
+        const int slot = atomicAdd(&wave_count[0], 1);
+        if (slot < kAddListCap) {
+          cand_key[slot] = e.x;
+          cand_corner[slot] = pack_corner(e.y, e.z);
+        }
+      }
     }
     __syncthreads();
-    add_list(m);
-  } else {
-    // ordered scan of all the metadata, 256 subgrids at a time
-    for (int base = 0; base < nr_subgrids; base += 256) {
-      const int s = base + tid;
-      bool hit = false;
-      int cx = 0, cy = 0;
-      if (s < nr_subgrids) {
-        const idg::Metadata m = metadata[s];
-        cx = m.coordinate.x;
-        cy = m.coordinate.y;
-        hit = fits(m, G, S, nr_w_layers) && m.coordinate.z == z &&
-              overlaps(cx, cy);
-      }
-      const unsigned long long mask = __ballot(hit);
-      __syncthreads();  // the previous chunk's list is consumed
-      if (lane == 0) wave_count[wave] = __popcll(mask);
-      __syncthreads();
-      int pos = 0, total = 0;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        pos += w < wave ? wave_count[w] : 0;
-        total += wave_count[w];
-      }
-      if (hit) {
-        pos += __popcll(mask & ((1ull << lane) - 1ull));  // ordered
-        keys[pos] = s;
-        corner[pos] = pack_corner(cx, cy);
-      }
-      __syncthreads();
-      add_list(total);
-    }
-  }
+    const int m = nrows <= kAddMaxRows ? wave_count[0] : kAddListCap + 1;
 
-  float2 *gz = grid + static_cast<size_t>(z) * 4 * G * G;
-#pragma unroll
-  for (int j = 0; j < kAddPix; ++j) {
-    const int i = tid + 256 * j;
-    const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
-    if (gx >= G || gy >= G) continue;
-#pragma unroll
-    for (int pol = 0; pol < 4; ++pol) {
-      float2 *o = gz + static_cast<size_t>(pol) * G * G +
-                  static_cast<size_t>(gy) * G + gx;
-      const float2 v = *o;
-      *o = make_float2(v.x + acc[j][pol].x, v.y + acc[j][pol].y);
+    // This workgroup's range [lo, hi) of the ordered list, and whether it
+    // is a segment of a crowded tile (partial tile, not the grid).
+    bool split = seg >= 1;
+    int base = he.w, nseg = he.z;
+    if (seg < 0 && sw.hdr != nullptr) {
+      // the tile's own workgroup: register a crowded tile (partial slots
+      // base .. base + nseg - 1), then count itself in
+      const bool crowd = nrows <= kAddMaxRows && m > kAddSegLen;
+      if (tid == 0) {
+        int ok = 0, hh = -1, b = 0, ns = 0;
+        if (crowd) {
+          ns = (m + kAddSegLen - 1) / kAddSegLen;
+          hh = atomicAdd(sw.hdr + kSegHeavy, 1);
+          b = atomicAdd(sw.hdr + kSegTotal, ns);
+          ok = hh < sw.heavy_cap && b + ns <= sw.slot_cap;  // (sized: always)
+          if (ok) {
+            sw.heavy[hh] = make_int4(tl, z, ns, b);
+            sw.done[hh] = 0;
+          }
+        }
+        bcast[0] = ok;
+        bcast[1] = hh;
+        bcast[2] = b;
+        bcast[3] = ns;
+      }
+      __syncthreads();
+      split = bcast[0] != 0;
+      h = bcast[1];
+      base = bcast[2];
+      nseg = bcast[3];
+      if (crowd)  // every reserved slot gets its owner (-1: not split)
+        for (int p = base + tid; p < min(base + nseg, sw.slot_cap); p += 256)
+          sw.owner[p] = split ? h : -1;
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) atomicAdd(sw.hdr + kSegMainDone, 1);
     }
+    if (seg < 0) seg = 0;
+    const int lo = split ? seg * kAddSegLen : 0;
+    const int hi = split ? lo + kAddSegLen : 0x7fffffff;
+
+    if (m <= kAddListCap) {
+      for (int i = tid; i < m; i += 256) {
+        const int k = cand_key[i];
+        int rank = 0;
+        for (int j = 0; j < m; ++j) rank += cand_key[j] < k;
+        keys[rank] = k;
+        corner[rank] = cand_corner[i];
+      }
+      __syncthreads();
+      add_list(lo, min(hi, m));
+    } else {
+      // ordered scan of all the metadata, 256 subgrids at a time, until
+      // the range is covered
+      int seen = 0;
+      for (int mb = 0; mb < nr_subgrids && seen < hi; mb += 256) {
+        const int s = mb + tid;
+        bool hit = false;
+        int cx = 0, cy = 0;
+        if (s < nr_subgrids) {
+          const idg::Metadata md = metadata[s];
+          cx = md.coordinate.x;
+          cy = md.coordinate.y;
+          hit = fits(md, G, S, nr_w_layers) && md.coordinate.z == z &&
+                overlaps(cx, cy);
+        }
+        const unsigned long long mask = __ballot(hit);
+        __syncthreads();  // the previous chunk's list is consumed
+        if (lane == 0) wave_count[wave] = __popcll(mask);
+        __syncthreads();
+        int pos = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          pos += w < wave ? wave_count[w] : 0;
+          total += wave_count[w];
+        }
+        if (hit) {
+          pos += __popcll(mask & ((1ull << lane) - 1ull));  // ordered
+          keys[pos] = s;
+          corner[pos] = pack_corner(cx, cy);
+        }
+        __syncthreads();
+        const int a = max(lo - seen, 0), b = min(hi - seen, total);
+        if (a < b) add_list(a, b);
+        seen += total;
+      }
+    }
+
+    float2 *gz = grid + static_cast<size_t>(z) * 4 * G * G;
+    if (!split) {
+#pragma unroll
+      for (int j = 0; j < kAddPix; ++j) {
+        const int i = tid + 256 * j;
+        const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
+        if (gx >= G || gy >= G) continue;
+#pragma unroll
+        for (int pol = 0; pol < 4; ++pol) {
+          float2 *o = gz + static_cast<size_t>(pol) * G * G +
+                      static_cast<size_t>(gy) * G + gx;
+          const float2 v = *o;
+          *o = make_float2(v.x + acc[j][pol].x, v.y + acc[j][pol].y);
+        }
+      }
+      return;
+    }
+    // a segment: partial slot base + seg; the last segment of the tile to
+    // finish adds the partials to the grid in segment order
+    float2 *pp = sw.partial + static_cast<size_t>(base + seg) * kAddPartialFloat2;
+#pragma unroll
+    for (int j = 0; j < kAddPix; ++j)
+#pragma unroll
+      for (int pol = 0; pol < 4; ++pol) pp[(j * 4 + pol) * 256 + tid] = acc[j][pol];
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) bcast[0] = atomicAdd(sw.done + h, 1) == nseg - 1;
+    __syncthreads();
+    if (bcast[0] == 0) return;
+    __threadfence();
+    const float2 *p0 = sw.partial + static_cast<size_t>(base) * kAddPartialFloat2;
+#pragma unroll
+    for (int j = 0; j < kAddPix; ++j) {
+      const int i = tid + 256 * j;
+      const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
+      if (gx >= G || gy >= G) continue;
+#pragma unroll
+      for (int pol = 0; pol < 4; ++pol) {
+        const int k = (j * 4 + pol) * 256 + tid;
+        float2 sum = p0[k];
+        for (int q = 1; q < nseg; ++q) {
+          const float2 v = p0[static_cast<size_t>(q) * kAddPartialFloat2 + k];
+          sum.x += v.x;
+          sum.y += v.y;
+        }
+        float2 *o = gz + static_cast<size_t>(pol) * G * G +
+                    static_cast<size_t>(gy) * G + gx;
+        const float2 v = *o;
+        *o = make_float2(v.x + sum.x, v.y + sum.y);
+      }
+    }
+  };
+
+  if (static_cast<int>(blockIdx.x) < ntiles) {
+    // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal
+    // neighbours, whose subgrid reads share cache lines, run on the same
+    // XCD's L2
+    add_tile(xcd_subgrid(blockIdx.x, ntiles), blockIdx.y, -1, -1,
+             make_int4(0, 0, 0, 0));
+    return;
+  }
+  // Segment workgroups: the last layer's row only, so every tile's
+  // workgroup is dispatched before any of them (each XCD dispatches its
+  // blocks in order; the tiles' workgroups wait on nothing).  They wait
+  // until every tile has counted itself in, then take partial slots.
+  if (sw.hdr == nullptr || blockIdx.y != gridDim.y - 1) return;
+  if (tid == 0) {
+    const int mains = ntiles * static_cast<int>(gridDim.y);
+    // (bounded: ~1 s, so that a broken invariant gives a wrong grid, which
+    // the tests see, rather than a hung device)
+    for (int spin = 0;
+         atomicAdd(sw.hdr + kSegMainDone, 0) < mains && spin < (1 << 22);
+         ++spin)
+      __builtin_amdgcn_s_sleep(8);
+    bcast[2] = min(atomicAdd(sw.hdr + kSegTotal, 0), sw.slot_cap);
+  }
+  __syncthreads();
+  __threadfence();
+  const int nslots = bcast[2];
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) bcast[1] = atomicAdd(sw.hdr + kSegTake, 1);
+    __syncthreads();
+    const int p = bcast[1];
+    if (p >= nslots) break;
+    const int h = load_agent(sw.owner + p);
+    if (h < 0) continue;
+    const int *hp = reinterpret_cast<const int *>(sw.heavy + h);
+    const int4 he = make_int4(load_agent(hp), load_agent(hp + 1),
+                              load_agent(hp + 2), load_agent(hp + 3));
+    if (p == he.w) continue;  // segment 0: the tile's own workgroup
+    add_tile(he.x, he.y, p - he.w, h, he);
+  }
+  // the last segment workgroup to leave zeroes the counters for the next
+  // launch (every tile's workgroup counted itself in before any of them
+  // started, and no slot is taken after this)
+  if (tid == 0 && atomicAdd(sw.hdr + kSegExit, 1) == nworkers - 1) {
+    sw.hdr[kSegHeavy] = 0;
+    sw.hdr[kSegTotal] = 0;
+    sw.hdr[kSegTake] = 0;
+    sw.hdr[kSegMainDone] = 0;
+    sw.hdr[kSegExit] = 0;
   }
 }
 
@@ -1059,14 +1262,47 @@ hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
   HomeSort hs;
   hipError_t err = home_sort(md, nr_subgrids, grid_size, subgrid_size,
                              nr_w_layers, stream, &hs);
+  // crowded tiles split into segments (IDG_ADD_SEG=0: one workgroup per
+  // tile whatever its list, the round-3 form)
+  const char *segenv = std::getenv("IDG_ADD_SEG");
+  const bool segmented = !(segenv != nullptr && segenv[0] == '0');
+  AdderSeg sw;
+  WorkspaceLease slease;
+  int nworkers = 0;
+  if (err == hipSuccess && segmented) {
+    const AdderSegCaps caps =
+        adder_seg_caps(nr_subgrids, subgrid_size, tg.ntx * tg.nty * nr_w_layers);
+    err = slease.acquire(stream, kWorkspaceAdderSeg, caps.bytes);
+    if (err == hipSuccess) {
+      char *b = static_cast<char *>(slease.ptr);
+      sw.heavy_cap = caps.heavy;
+      sw.slot_cap = caps.slots;
+      sw.hdr = reinterpret_cast<int *>(b);
+      b += kSegHdrInts * sizeof(int);
+      sw.partial = reinterpret_cast<float2 *>(b);
+      b += static_cast<size_t>(caps.slots) * kAddPartialFloat2 * sizeof(float2);
+      sw.heavy = reinterpret_cast<int4 *>(b);
+      b += static_cast<size_t>(caps.heavy) * sizeof(int4);
+      sw.done = reinterpret_cast<int *>(b);
+      b += static_cast<size_t>(caps.heavy) * sizeof(int);
+      sw.owner = reinterpret_cast<int *>(b);
+      // zero when new or after a failed launch; else left zero by the
+      // last segment workgroup
+      if (!slease.clean)
+        err = hipMemsetAsync(sw.hdr, 0, kSegHdrInts * sizeof(int), stream);
+      nworkers = kAddWorkers;
+    }
+  }
   if (err == hipSuccess) {
-    hipLaunchKernelGGL(kernel_adder, dim3(tg.ntx * tg.nty, nr_w_layers),
+    hipLaunchKernelGGL(kernel_adder,
+                       dim3(tg.ntx * tg.nty + nworkers, nr_w_layers),
                        dim3(256), 0, stream, md, nr_subgrids, hs.offset,
                        hs.order, static_cast<const float2 *>(d_subgrids),
                        static_cast<float2 *>(d_grid), grid_size,
-                       subgrid_size, nr_w_layers);
+                       subgrid_size, nr_w_layers, sw, nworkers);
     err = hipGetLastError();
   }
+  slease.leave_clean = err == hipSuccess && nworkers > 0;
   return free_home_sort(hs, err, stream);
 }
 

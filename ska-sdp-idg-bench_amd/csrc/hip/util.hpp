@@ -152,7 +152,8 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
 // leave_clean set (its contents are what that sequence left).  While another
 // host thread holds the slot, ptr is a private stream-ordered allocation
 // (never clean) freed after the sequence.
-constexpr int kWorkspaceQueue = 0, kWorkspaceHomeSort = 1;
+constexpr int kWorkspaceQueue = 0, kWorkspaceHomeSort = 1,
+              kWorkspaceAdderSeg = 2;
 struct WorkspaceLease {
   void *ptr = nullptr;
   hipStream_t stream = nullptr;
