@@ -645,11 +645,15 @@ __global__ void __launch_bounds__(256)
       h = bcast[1];
       base = bcast[2];
       nseg = bcast[3];
-      if (crowd)  // every reserved slot gets its owner (-1: not split)
+      if (crowd) {
+        // every reserved slot gets its owner (-1: not split), published
+        // before the count (a release fence writes back this XCD's L2, so
+        // only a crowded tile pays for one)
         for (int p = base + tid; p < min(base + nseg, sw.slot_cap); p += 256)
           sw.owner[p] = split ? h : -1;
-      __threadfence();
-      __syncthreads();
+        __threadfence();
+        __syncthreads();
+      }
       if (tid == 0) atomicAdd(sw.hdr + kSegMainDone, 1);
     }
     if (seg < 0) seg = 0;
@@ -773,15 +777,19 @@ __global__ void __launch_bounds__(256)
     const int mains = ntiles * static_cast<int>(gridDim.y);
     // (bounded: ~1 s, so that a broken invariant gives a wrong grid, which
     // the tests see, rather than a hung device)
+    // (a plain device-scope load per poll, not an atomic RMW: 256 pollers
+    // on one address would contend with the tiles' own counting)
     for (int spin = 0;
-         atomicAdd(sw.hdr + kSegMainDone, 0) < mains && spin < (1 << 22);
+         load_agent(sw.hdr + kSegMainDone) < mains && spin < (1 << 18);
          ++spin)
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(64);
     bcast[2] = min(atomicAdd(sw.hdr + kSegTotal, 0), sw.slot_cap);
   }
   __syncthreads();
-  __threadfence();
   const int nslots = bcast[2];
+  // acquire what the crowded tiles published (an acquire fence invalidates
+  // this XCD's L2 under the tiles still running: none when nothing split)
+  if (nslots > 0) __threadfence();
   for (;;) {
     __syncthreads();
     if (tid == 0) bcast[1] = atomicAdd(sw.hdr + kSegTake, 1);
