@@ -403,35 +403,42 @@ __global__ void __launch_bounds__(1024)
 //
 // Crowded tiles (round 4): one workgroup per tile serialises a crowded uv
 // centre onto a few CUs (24,500 subgrids around the centre: 0.2 -> 6.6 ms,
-// DESIGN.md §11).  A tile whose ordered list holds more than kAddSegLen
-// entries is cut into segments of kAddSegLen: its own workgroup sums the
-// first into a partial tile, kAddWorkers workgroups launched after the
-// tiles sum the others (taking the partial slots from a counter), and the
-// workgroup that finishes a tile's last segment adds the partials to the
-// grid in segment order.  Deterministic (a segment's sum and the order of
-// the partials depend on the data only); a tile with at most kAddSegLen
-// entries takes the single-workgroup path unchanged, bit for bit.
+// DESIGN.md §11).  A tile whose candidate rows hold more than kAddSegLen
+// subgrids (an upper bound of its list, from the home sort's offsets
+// alone) is summed in segments of kAddSegLen list entries instead, in
+// three launches that need no cross-workgroup waits or fences (each kernel
+// boundary orders the next one's reads):
+//   kernel_adder_crowd   one thread per tile: the crowded tiles, their
+//                        segment count and partial slots;
+//   kernel_adder         the segment workgroups first in the grid (so they
+//                        start at once), each segment into its own partial
+//                        tile; then one workgroup per uncrowded tile, as
+//                        before and bit for bit;
+//   kernel_adder_combine each crowded tile's partials added to the grid in
+//                        segment order.
+// Deterministic: a segment's sum and the order of the partials depend on
+// the data only.
 constexpr int kAddSegLen = 256;   // list entries per segment
-constexpr int kAddWorkers = 256;  // segment workgroups after the tiles
-// counters, each on its own 128-byte line; zero between launches
-constexpr int kSegHeavy = 0, kSegTotal = 32, kSegTake = 64, kSegMainDone = 96,
-              kSegExit = 128, kSegHdrInts = 160;
+constexpr int kAddWorkers = 256;  // segment workgroups
+constexpr int kAddCombiners = 64;
+// counters, each on its own 128-byte line; zero between launches (the
+// combine kernel's last workgroup clears them)
+constexpr int kSegHeavy = 0, kSegTotal = 32, kSegExit = 64, kSegHdrInts = 96;
 constexpr size_t kAddPartialFloat2 = static_cast<size_t>(kAddPix) * 4 * 256;
 
 // The segment workspace (util.hpp WorkspaceLease, cached per stream):
 // counters | partial [slot][pixel j][pol][thread] | heavy {tile, z, nseg,
-// base} | done (segments finished per crowded tile) | owner (crowded tile
-// of each partial slot).  Sized for the worst case of the batch, so that
-// no tile is ever refused (which tiles split must not depend on the order
-// of the atomics): a subgrid overlaps at most tps tiles, so the lists hold
-// at most T = nr_subgrids * tps entries, at most T / kAddSegLen tiles are
-// crowded, and their segments number at most 2 T / kAddSegLen.
+// base} | owner (crowded tile of each partial slot) | tile_seg (per tile:
+// its crowded index, or -1).  Sized for the worst case of the batch: a
+// subgrid is a candidate of at most tps tiles, so the bounds sum to at most
+// T = nr_subgrids * tps, at most T / kAddSegLen tiles are crowded, and
+// their segments number at most 2 T / kAddSegLen + 1.
 struct AdderSeg {
   int *hdr = nullptr;
   float2 *partial = nullptr;
   int4 *heavy = nullptr;
-  int *done = nullptr;
   int *owner = nullptr;
+  int *tile_seg = nullptr;
   int heavy_cap = 0, slot_cap = 0;
 };
 
@@ -442,7 +449,8 @@ struct AdderSegCaps {
 inline AdderSegCaps adder_seg_caps(int nr_subgrids, int S, int ntiles_all) {
   const long long cols_x = (S - 1 + kTW - 1) / kTW + 1;
   const long long cols_y = (S - 1 + kTH - 1) / kTH + 1;
-  const long long entries = static_cast<long long>(nr_subgrids) * cols_x * cols_y;
+  const long long entries =
+      static_cast<long long>(nr_subgrids) * cols_x * cols_y;
   const long long per = (entries + kAddSegLen - 1) / kAddSegLen;
   AdderSegCaps c;
   c.heavy = static_cast<int>(std::min<long long>(ntiles_all, per + 1));
@@ -450,14 +458,85 @@ inline AdderSegCaps adder_seg_caps(int nr_subgrids, int S, int ntiles_all) {
   c.bytes = kSegHdrInts * sizeof(int) +
             static_cast<size_t>(c.slots) *
                 (kAddPartialFloat2 * sizeof(float2) + sizeof(int)) +
-            static_cast<size_t>(c.heavy) * (sizeof(int4) + sizeof(int));
+            static_cast<size_t>(c.heavy) * sizeof(int4) +
+            static_cast<size_t>(ntiles_all) * sizeof(int);
   return c;
 }
 
-// relaxed device-scope loads of what other workgroups of the launch wrote
-// (after the acquire fence that follows their counter)
-__device__ __forceinline__ int load_agent(const int *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ void __launch_bounds__(256)
+    kernel_adder_crowd(const int *__restrict__ offset, int G, int S,
+                       int nr_w_layers, AdderSeg sw) {
+  const TileGrid tg(G);
+  const int ntiles = tg.ntx * tg.nty;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= ntiles * nr_w_layers) return;
+  const int z = t / ntiles, tl = t - z * ntiles;
+  const int tx = tl % tg.ntx, ty = tl / tg.ntx;
+  const int DX = (S - 1 + kTW - 1) / kTW, DY = (S - 1 + kTH - 1) / kTH;
+  const int nrows = min(DY, ty) + 1;
+  const int hx0 = max(0, tx - DX);
+  int bound = 0;
+  if (nrows <= kAddMaxRows)
+    for (int r = 0; r < nrows; ++r) {
+      const int k0 = (z * tg.nty + ty - r) * tg.ntx;
+      bound += offset[k0 + tx + 1] - offset[k0 + hx0];
+    }
+  int h = -1;
+  if (bound > kAddSegLen) {
+    const int ns = (bound + kAddSegLen - 1) / kAddSegLen;
+    h = atomicAdd(sw.hdr + kSegHeavy, 1);
+    const int b = atomicAdd(sw.hdr + kSegTotal, ns);
+    if (h < sw.heavy_cap && b + ns <= sw.slot_cap) {  // (sized: always)
+      sw.heavy[h] = make_int4(tl, z, ns, b);
+      for (int s = 0; s < ns; ++s) sw.owner[b + s] = h;
+    } else {
+      h = -1;
+    }
+  }
+  sw.tile_seg[t] = h;
+}
+
+// Each crowded tile's partials, in segment order, onto the grid; the last
+// workgroup to finish clears the counters for the next launch.
+__global__ void __launch_bounds__(256)
+    kernel_adder_combine(float2 *__restrict__ grid, int G, AdderSeg sw) {
+  const int tid = threadIdx.x;
+  const TileGrid tg(G);
+  const int nh = min(sw.hdr[kSegHeavy], sw.heavy_cap);
+  for (int h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int4 he = sw.heavy[h];  // {tile, z, nseg, base}
+    const int tx0 = (he.x % tg.ntx) * kTW, ty0 = (he.x / tg.ntx) * kTH;
+    float2 *gz = grid + static_cast<size_t>(he.y) * 4 * G * G;
+    const float2 *p0 =
+        sw.partial + static_cast<size_t>(he.w) * kAddPartialFloat2;
+#pragma unroll
+    for (int j = 0; j < kAddPix; ++j) {
+      const int i = tid + 256 * j;
+      const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
+      if (gx >= G || gy >= G) continue;
+#pragma unroll
+      for (int pol = 0; pol < 4; ++pol) {
+        const int k = (j * 4 + pol) * 256 + tid;
+        float2 sum = p0[k];
+        for (int q = 1; q < he.z; ++q) {
+          const float2 v = p0[static_cast<size_t>(q) * kAddPartialFloat2 + k];
+          sum.x += v.x;
+          sum.y += v.y;
+        }
+        float2 *o = gz + static_cast<size_t>(pol) * G * G +
+                    static_cast<size_t>(gy) * G + gx;
+        const float2 v = *o;
+        *o = make_float2(v.x + sum.x, v.y + sum.y);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && atomicAdd(sw.hdr + kSegExit, 1) ==
+                      static_cast<int>(gridDim.x) - 1) {
+    sw.hdr[kSegHeavy] = 0;
+    sw.hdr[kSegTotal] = 0;
+    sw.hdr[kSegExit] = 0;
+  }
 }
 
 __global__ void __launch_bounds__(256)
@@ -473,7 +552,6 @@ __global__ void __launch_bounds__(256)
   __shared__ int cand_key[kAddListCap], cand_corner[kAddListCap];
   __shared__ int row_begin[kAddMaxRows], row_pre[kAddMaxRows + 1];
   __shared__ int wave_count[4];
-  __shared__ int bcast[4];
   __shared__ float2 table[kAddMaxTable];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TileGrid tg(G);
@@ -485,10 +563,9 @@ __global__ void __launch_bounds__(256)
     for (int k = tid; k < 2 * S - 1; k += 256)
       table[k] = unit_phasor(k * (S + 1) - S, 2 * S, 1.0f);
 
-  // Tile tl of layer z.  seg < 0: the tile's own workgroup (the whole list,
-  // or its first segment when crowded); seg >= 1: that segment of crowded
-  // tile h (heavy entry he).
-  auto add_tile = [&](int tl, int z, int seg, int h, int4 he) {
+  // Tile tl of layer z: the whole list onto the grid (seg < 0), or list
+  // entries [seg kAddSegLen, (seg + 1) kAddSegLen) into partial slot `slot`.
+  auto add_tile = [&](int tl, int z, int seg, int slot) {
     const int tx = tl % tg.ntx, ty = tl / tg.ntx;
     const int tx0 = tx * kTW, ty0 = ty * kTH;
 
@@ -615,48 +692,7 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
     const int m = nrows <= kAddMaxRows ? wave_count[0] : kAddListCap + 1;
 
-    // This workgroup's range [lo, hi) of the ordered list, and whether it
-    // is a segment of a crowded tile (partial tile, not the grid).
-    bool split = seg >= 1;
-    int base = he.w, nseg = he.z;
-    if (seg < 0 && sw.hdr != nullptr) {
-      // the tile's own workgroup: register a crowded tile (partial slots
-      // base .. base + nseg - 1), then count itself in
-      const bool crowd = nrows <= kAddMaxRows && m > kAddSegLen;
-      if (tid == 0) {
-        int ok = 0, hh = -1, b = 0, ns = 0;
-        if (crowd) {
-          ns = (m + kAddSegLen - 1) / kAddSegLen;
-          hh = atomicAdd(sw.hdr + kSegHeavy, 1);
-          b = atomicAdd(sw.hdr + kSegTotal, ns);
-          ok = hh < sw.heavy_cap && b + ns <= sw.slot_cap;  // (sized: always)
-          if (ok) {
-            sw.heavy[hh] = make_int4(tl, z, ns, b);
-            sw.done[hh] = 0;
-          }
-        }
-        bcast[0] = ok;
-        bcast[1] = hh;
-        bcast[2] = b;
-        bcast[3] = ns;
-      }
-      __syncthreads();
-      split = bcast[0] != 0;
-      h = bcast[1];
-      base = bcast[2];
-      nseg = bcast[3];
-      if (crowd) {
-        // every reserved slot gets its owner (-1: not split), published
-        // before the count (a release fence writes back this XCD's L2, so
-        // only a crowded tile pays for one)
-        for (int p = base + tid; p < min(base + nseg, sw.slot_cap); p += 256)
-          sw.owner[p] = split ? h : -1;
-        __threadfence();
-        __syncthreads();
-      }
-      if (tid == 0) atomicAdd(sw.hdr + kSegMainDone, 1);
-    }
-    if (seg < 0) seg = 0;
+    const bool split = seg >= 0;
     const int lo = split ? seg * kAddSegLen : 0;
     const int hi = split ? lo + kAddSegLen : 0x7fffffff;
 
@@ -724,96 +760,32 @@ __global__ void __launch_bounds__(256)
       }
       return;
     }
-    // a segment: partial slot base + seg; the last segment of the tile to
-    // finish adds the partials to the grid in segment order
-    float2 *pp = sw.partial + static_cast<size_t>(base + seg) * kAddPartialFloat2;
+    // a segment: its partial tile (kernel_adder_combine adds the partials)
+    float2 *pp = sw.partial + static_cast<size_t>(slot) * kAddPartialFloat2;
 #pragma unroll
     for (int j = 0; j < kAddPix; ++j)
 #pragma unroll
-      for (int pol = 0; pol < 4; ++pol) pp[(j * 4 + pol) * 256 + tid] = acc[j][pol];
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) bcast[0] = atomicAdd(sw.done + h, 1) == nseg - 1;
-    __syncthreads();
-    if (bcast[0] == 0) return;
-    __threadfence();
-    const float2 *p0 = sw.partial + static_cast<size_t>(base) * kAddPartialFloat2;
-#pragma unroll
-    for (int j = 0; j < kAddPix; ++j) {
-      const int i = tid + 256 * j;
-      const int gx = tx0 + (i & (kTW - 1)), gy = ty0 + i / kTW;
-      if (gx >= G || gy >= G) continue;
-#pragma unroll
-      for (int pol = 0; pol < 4; ++pol) {
-        const int k = (j * 4 + pol) * 256 + tid;
-        float2 sum = p0[k];
-        for (int q = 1; q < nseg; ++q) {
-          const float2 v = p0[static_cast<size_t>(q) * kAddPartialFloat2 + k];
-          sum.x += v.x;
-          sum.y += v.y;
-        }
-        float2 *o = gz + static_cast<size_t>(pol) * G * G +
-                    static_cast<size_t>(gy) * G + gx;
-        const float2 v = *o;
-        *o = make_float2(v.x + sum.x, v.y + sum.y);
-      }
-    }
+      for (int pol = 0; pol < 4; ++pol)
+        pp[(j * 4 + pol) * 256 + tid] = acc[j][pol];
   };
 
-  if (static_cast<int>(blockIdx.x) < ntiles) {
-    // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal
-    // neighbours, whose subgrid reads share cache lines, run on the same
-    // XCD's L2
-    add_tile(xcd_subgrid(blockIdx.x, ntiles), blockIdx.y, -1, -1,
-             make_int4(0, 0, 0, 0));
+  // segment workgroups first (kernel_adder_crowd listed the slots before
+  // this launch), one per slot in turn; layer row 0 only
+  if (static_cast<int>(blockIdx.x) < nworkers) {
+    if (blockIdx.y != 0) return;
+    const int total = min(sw.hdr[kSegTotal], sw.slot_cap);
+    for (int p = blockIdx.x; p < total; p += nworkers) {
+      const int4 he = sw.heavy[sw.owner[p]];  // {tile, z, nseg, base}
+      add_tile(he.x, he.y, p - he.w, p);
+    }
     return;
   }
-  // Segment workgroups: the last layer's row only, so every tile's
-  // workgroup is dispatched before any of them (each XCD dispatches its
-  // blocks in order; the tiles' workgroups wait on nothing).  They wait
-  // until every tile has counted itself in, then take partial slots.
-  if (sw.hdr == nullptr || blockIdx.y != gridDim.y - 1) return;
-  if (tid == 0) {
-    const int mains = ntiles * static_cast<int>(gridDim.y);
-    // (bounded: ~1 s, so that a broken invariant gives a wrong grid, which
-    // the tests see, rather than a hung device)
-    // (a plain device-scope load per poll, not an atomic RMW: 256 pollers
-    // on one address would contend with the tiles' own counting)
-    for (int spin = 0;
-         load_agent(sw.hdr + kSegMainDone) < mains && spin < (1 << 18);
-         ++spin)
-      __builtin_amdgcn_s_sleep(64);
-    bcast[2] = min(atomicAdd(sw.hdr + kSegTotal, 0), sw.slot_cap);
-  }
-  __syncthreads();
-  const int nslots = bcast[2];
-  // acquire what the crowded tiles published (an acquire fence invalidates
-  // this XCD's L2 under the tiles still running: none when nothing split)
-  if (nslots > 0) __threadfence();
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) bcast[1] = atomicAdd(sw.hdr + kSegTake, 1);
-    __syncthreads();
-    const int p = bcast[1];
-    if (p >= nslots) break;
-    const int h = load_agent(sw.owner + p);
-    if (h < 0) continue;
-    const int *hp = reinterpret_cast<const int *>(sw.heavy + h);
-    const int4 he = make_int4(load_agent(hp), load_agent(hp + 1),
-                              load_agent(hp + 2), load_agent(hp + 3));
-    if (p == he.w) continue;  // segment 0: the tile's own workgroup
-    add_tile(he.x, he.y, p - he.w, h, he);
-  }
-  // the last segment workgroup to leave zeroes the counters for the next
-  // launch (every tile's workgroup counted itself in before any of them
-  // started, and no slot is taken after this)
-  if (tid == 0 && atomicAdd(sw.hdr + kSegExit, 1) == nworkers - 1) {
-    sw.hdr[kSegHeavy] = 0;
-    sw.hdr[kSegTotal] = 0;
-    sw.hdr[kSegTake] = 0;
-    sw.hdr[kSegMainDone] = 0;
-    sw.hdr[kSegExit] = 0;
-  }
+  // XCD-contiguous tiles (device.hpp: xcd_subgrid): horizontal neighbours,
+  // whose subgrid reads share cache lines, run on the same XCD's L2
+  const int tl = xcd_subgrid(blockIdx.x - nworkers, ntiles);
+  if (nworkers > 0 && sw.tile_seg[blockIdx.y * ntiles + tl] >= 0)
+    return;  // crowded: its segments and kernel_adder_combine
+  add_tile(tl, blockIdx.y, -1, 0);
 }
 
 // F[s][pol][ys][xs] = conj(shift_phasor(x, y)) * grid[z][pol][cy + y][cx + x]
@@ -1291,23 +1263,36 @@ hipError_t launch_adder(int nr_subgrids, int grid_size, int subgrid_size,
       b += static_cast<size_t>(caps.slots) * kAddPartialFloat2 * sizeof(float2);
       sw.heavy = reinterpret_cast<int4 *>(b);
       b += static_cast<size_t>(caps.heavy) * sizeof(int4);
-      sw.done = reinterpret_cast<int *>(b);
-      b += static_cast<size_t>(caps.heavy) * sizeof(int);
       sw.owner = reinterpret_cast<int *>(b);
-      // zero when new or after a failed launch; else left zero by the
-      // last segment workgroup
+      b += static_cast<size_t>(caps.slots) * sizeof(int);
+      sw.tile_seg = reinterpret_cast<int *>(b);
+      // zero when new or after a failed launch; else left zero by
+      // kernel_adder_combine's last workgroup
       if (!slease.clean)
         err = hipMemsetAsync(sw.hdr, 0, kSegHdrInts * sizeof(int), stream);
       nworkers = kAddWorkers;
     }
   }
+  const int ntiles_all = tg.ntx * tg.nty * nr_w_layers;
+  if (err == hipSuccess && nworkers > 0) {
+    hipLaunchKernelGGL(kernel_adder_crowd, dim3((ntiles_all + 255) / 256),
+                       dim3(256), 0, stream, hs.offset, grid_size,
+                       subgrid_size, nr_w_layers, sw);
+    err = hipGetLastError();
+  }
   if (err == hipSuccess) {
     hipLaunchKernelGGL(kernel_adder,
-                       dim3(tg.ntx * tg.nty + nworkers, nr_w_layers),
+                       dim3(nworkers + tg.ntx * tg.nty, nr_w_layers),
                        dim3(256), 0, stream, md, nr_subgrids, hs.offset,
                        hs.order, static_cast<const float2 *>(d_subgrids),
                        static_cast<float2 *>(d_grid), grid_size,
                        subgrid_size, nr_w_layers, sw, nworkers);
+    err = hipGetLastError();
+  }
+  if (err == hipSuccess && nworkers > 0) {
+    hipLaunchKernelGGL(kernel_adder_combine, dim3(kAddCombiners), dim3(256),
+                       0, stream, static_cast<float2 *>(d_grid), grid_size,
+                       sw);
     err = hipGetLastError();
   }
   slease.leave_clean = err == hipSuccess && nworkers > 0;
