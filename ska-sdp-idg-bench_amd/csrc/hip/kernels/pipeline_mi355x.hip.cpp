@@ -486,12 +486,13 @@ __global__ void __launch_bounds__(256)
     const int ns = (bound + kAddSegLen - 1) / kAddSegLen;
     h = atomicAdd(sw.hdr + kSegHeavy, 1);
     const int b = atomicAdd(sw.hdr + kSegTotal, ns);
-    if (h < sw.heavy_cap && b + ns <= sw.slot_cap) {  // (sized: always)
-      sw.heavy[h] = make_int4(tl, z, ns, b);
-      for (int s = 0; s < ns; ++s) sw.owner[b + s] = h;
-    } else {
-      h = -1;
-    }
+    const bool ok = h < sw.heavy_cap && b + ns <= sw.slot_cap;  // (sized: always)
+    if (ok) sw.heavy[h] = make_int4(tl, z, ns, b);
+    // every slot below the total gets an owner (-1: skipped by the segment
+    // workgroups; the tile then takes the one-workgroup path)
+    for (int s = 0; s < ns && b + s < sw.slot_cap; ++s)
+      sw.owner[b + s] = ok ? h : -1;
+    if (!ok) h = -1;
   }
   sw.tile_seg[t] = h;
 }
@@ -775,7 +776,9 @@ __global__ void __launch_bounds__(256)
     if (blockIdx.y != 0) return;
     const int total = min(sw.hdr[kSegTotal], sw.slot_cap);
     for (int p = blockIdx.x; p < total; p += nworkers) {
-      const int4 he = sw.heavy[sw.owner[p]];  // {tile, z, nseg, base}
+      const int h = sw.owner[p];
+      if (h < 0) continue;
+      const int4 he = sw.heavy[h];  // {tile, z, nseg, base}
       add_tile(he.x, he.y, p - he.w, p);
     }
     return;
