@@ -21,10 +21,29 @@
  *   degridder phase_index  = fma(u, l, v*m) + w*n
  *             phase_offset = fma(u_o, l, v_o*m) + w_o*n
  *             phase        = fma(phase_index, k, -phase_offset)
- *   complex a*b            = (fma(ar, br, -(ai*bi)), fma(ar, bi, ai*br))
+ *   complex a*b            re = fma(ar, br, -(ai*bi)) at every site;
+ *                          im = fma(ar, bi, ai*br)  (cmul_a) or
+ *                               fma(ai, br, ar*bi)  (cmul_b), per site:
+ *     gridder   vis * phasor (gridder_reference.cpp:79)           cmul_b
+ *               A1^H * P, c[0], c[1] and the c[0], c[1] updates   cmul_a
+ *               A1^H * P, c[2], c[3] and their updates            cmul_b
+ *               (A1^H P) * A2, all eight products                 cmul_b
+ *     degridder A1 * P (degridder_reference.cpp:71), all eight    cmul_a
+ *               (A1 P) * A2^H, all eight products                 cmul_b
+ *               pixel * phasor (degridder_reference.cpp:114)      cmul_b
+ *   The im form differs by site because GCC picks which of the two products
+ *   to keep in the FMA per expression.  Each site was pinned by flipping it
+ *   alone against the golden outputs (every other choice loses 3-80% of the
+ *   bit-equal outputs); two degridder sites (A1 * P c[0], c[2]) multiply a
+ *   pol-0 pixel whose imaginary part is 0 in the reference's synthetic
+ *   subgrids, where both forms agree, and take the form of the other six
+ *   products of that matrix product.  (Round 1-4 used cmul_a everywhere:
+ *   2e-7 from the reference, 30% of outputs bit-equal.)
  *   n: tmp                 = fma(l, l, m*m)
- * Pinned by tests/test_oracle.py against tests/golden/ (generated from the
- * reference's own CPU path, oracle/make_golden.sh).
+ * With these the restatement is BIT-EXACT to the reference on every golden
+ * case (tests/test_oracle.py), given the same libm sincosf (glibc; the GPU
+ * box runs this image).  Pinned against tests/golden/ (generated from the
+ * reference's own CPU path, tests/golden/make_golden.py).
  */
 #include "idg_oracle.h"
 
@@ -42,10 +61,18 @@ typedef struct {
   float re, im;
 } cf;
 
-static inline cf cmul(cf a, cf b) {
+/* The two forms GCC gave std::complex<float> a*b (header comment). */
+static inline cf cmul_a(cf a, cf b) {
   cf r;
   r.re = fmaf(a.re, b.re, -(a.im * b.im));
   r.im = fmaf(a.re, b.im, a.im * b.re);
+  return r;
+}
+
+static inline cf cmul_b(cf a, cf b) {
+  cf r;
+  r.re = fmaf(a.re, b.re, -(a.im * b.im));
+  r.im = fmaf(a.im, b.re, a.re * b.im);
   return r;
 }
 
@@ -66,16 +93,23 @@ static inline float n_of(float l, float m) {
   return tmp > 1.0 ? 1.0f : tmp / (1.0f + sqrtf(1.0f - tmp));
 }
 
-/* 2x2 complex product c = a*b, same accumulation order as math.hpp:26-37. */
-static inline void jones_mul(const cf *a, const cf *b, cf *c) {
-  c[0] = cmul(a[0], b[0]);
-  c[1] = cmul(a[0], b[1]);
-  c[2] = cmul(a[2], b[0]);
-  c[3] = cmul(a[2], b[1]);
-  c[0] = cadd(c[0], cmul(a[1], b[2]));
-  c[1] = cadd(c[1], cmul(a[1], b[3]));
-  c[2] = cadd(c[2], cmul(a[3], b[2]));
-  c[3] = cadd(c[3], cmul(a[3], b[3]));
+/* 2x2 complex product c = a*b, same accumulation order as math.hpp:26-37;
+ * form_top / form_bottom: the complex-product form (0 = cmul_a, 1 = cmul_b)
+ * of rows c[0], c[1] and c[2], c[3]. */
+static inline cf cmul_f(cf a, cf b, int form) {
+  return form ? cmul_b(a, b) : cmul_a(a, b);
+}
+
+static inline void jones_mul(const cf *a, const cf *b, cf *c, int form_top,
+                             int form_bottom) {
+  c[0] = cmul_f(a[0], b[0], form_top);
+  c[1] = cmul_f(a[0], b[1], form_top);
+  c[2] = cmul_f(a[2], b[0], form_bottom);
+  c[3] = cmul_f(a[2], b[1], form_bottom);
+  c[0] = cadd(c[0], cmul_f(a[1], b[2], form_top));
+  c[1] = cadd(c[1], cmul_f(a[1], b[3], form_top));
+  c[2] = cadd(c[2], cmul_f(a[3], b[2], form_bottom));
+  c[3] = cadd(c[3], cmul_f(a[3], b[3], form_bottom));
 }
 
 /* conjugate transpose (math.hpp:39-63) */
@@ -151,7 +185,7 @@ static void gridder_one(int s, int grid_size, int subgrid_size,
           cf phasor = {cosf(phase), sinf(phase)};
           const cf *v4 = vis + (row * nr_channels + c) * NCORR;
           for (int p = 0; p < NCORR; p++)
-            pix[p] = cadd(pix[p], cmul(v4[p], phasor));
+            pix[p] = cadd(pix[p], cmul_b(v4[p], phasor));
         }
       }
       /* A-term: P = A1^H * P * A2 (math.hpp:65-77) */
@@ -161,8 +195,8 @@ static void gridder_one(int s, int grid_size, int subgrid_size,
                               g.station2, y, x);
       cf a1h[4], tmp[4];
       jones_herm(a1, a1h);
-      jones_mul(a1h, pix, tmp);
-      jones_mul(tmp, a2, pix);
+      jones_mul(a1h, pix, tmp, 0, 1);
+      jones_mul(tmp, a2, pix, 1, 1);
       const float sph = spheroidal[y * S + x];
       for (int p = 0; p < NCORR; p++) {
         cf *dst = subgrids + (((size_t)s * NCORR + p) * S + y) * S + x;
@@ -216,9 +250,9 @@ static void degridder_one(int s, int grid_size, int subgrid_size,
                               g.station1, y, x);
       const cf *a2 = aterm_at(aterms, nr_stations, S, g.aterm_index,
                               g.station2, y, x);
-      jones_mul(a1, p, tmp);
+      jones_mul(a1, p, tmp, 0, 0);
       jones_herm(a2, a2h);
-      jones_mul(tmp, a2h, pixels + ((size_t)y * S + x) * NCORR);
+      jones_mul(tmp, a2h, pixels + ((size_t)y * S + x) * NCORR, 1, 1);
     }
   }
   /* degridder_reference.cpp:82-127 */
@@ -243,7 +277,7 @@ static void degridder_one(int s, int grid_size, int subgrid_size,
           cf phasor = {cosf(phase), sinf(phase)};
           const cf *px = pixels + ((size_t)y * S + x) * NCORR;
           for (int p = 0; p < NCORR; p++)
-            sum[p] = cadd(sum[p], cmul(px[p], phasor));
+            sum[p] = cadd(sum[p], cmul_b(px[p], phasor));
         }
       }
       cf *dst = vis + (row * nr_channels + c) * NCORR;

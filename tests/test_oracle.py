@@ -42,6 +42,37 @@ def test_oracle_matches_reference_golden(oracle_lib, case):
     assert ed < ORACLE_BAR, f"degridder {case}: {ed}"
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_bit_exact_to_reference_golden(oracle_lib, case):
+    # with GCC's per-site complex-product forms (idg_oracle.c header) the
+    # restatement computes the reference's bits, not just its values: every
+    # output of every golden case, both directions (same glibc sincosf)
+    p, a = load_case(case)
+    g, d = _run(oracle_lib, p, a)
+    assert np.array_equal(g, a["gridder_out"]), case
+    assert np.array_equal(d, a["degridder_out"]), case
+
+
+@pytest.mark.skipif(not orc.Reference.available(portable=True),
+                    reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_bit_exact_to_reference_at_T128_C256(oracle_lib):
+    # the -c NR_CHANNELS=256 shape (T x C = 32,768 sequential adds per pixel)
+    # that the reference's own build is 1.27e-5 from exact at
+    import idg_amd
+    a = idg_amd.generate(2, 2, 128, 256, 1024, 32, nthreads=8)
+    ns = a["metadata"].size
+    args = (ns, 1024, 32, idg_amd.IMAGE_SIZE, 0.0, 256, 2)
+    ref, ours = orc.Reference(portable=True), np.zeros((ns, 4, 32, 32, 2),
+                                                       np.float32)
+    r = np.zeros_like(ours)
+    ref.gridder(*args, a["uvw"], a["wavenumbers"], a["visibilities"],
+                a["spheroidal"], a["aterms"], a["metadata"], r)
+    oracle_lib.gridder(*args, a["uvw"], a["wavenumbers"], a["visibilities"],
+                       a["spheroidal"], a["aterms"], a["metadata"], ours,
+                       nthreads=8)
+    assert np.array_equal(ours, r)
+
+
 def test_oracle_multithreaded_identical(oracle_lib):
     p, a = load_case("multi")
     ns, G, S = p["nr_subgrids"], p["grid_size"], p["subgrid_size"]
