@@ -42,8 +42,16 @@ struct cfloat {
   float re, im;
 };
 
-IDG_HD inline cfloat cmul(cfloat a, cfloat b) {
+// a * b as GCC compiled the reference's std::complex<float> products: the
+// real part always fma(ar, br, -(ai*bi)); the imaginary part keeps one of the
+// two products in the FMA, chosen per expression (oracle/idg_oracle.c header:
+// each site pinned bit for bit against the reference's own outputs).
+IDG_HD inline cfloat cmul(cfloat a, cfloat b) {  // form a
   return {fmaf(a.re, b.re, -(a.im * b.im)), fmaf(a.re, b.im, a.im * b.re)};
+}
+
+IDG_HD inline cfloat cmul_b(cfloat a, cfloat b) {  // form b
+  return {fmaf(a.re, b.re, -(a.im * b.im)), fmaf(a.im, b.re, a.re * b.im)};
 }
 
 IDG_HD inline cfloat cadd(cfloat a, cfloat b) {
@@ -52,12 +60,23 @@ IDG_HD inline cfloat cadd(cfloat a, cfloat b) {
 
 IDG_HD inline cfloat cconj(cfloat a) { return {a.re, -a.im}; }
 
-// c = a * b for 2x2 matrices stored {xx, xy, yx, yy}.
+// c = a * b for 2x2 matrices stored {xx, xy, yx, yy}, in the order of
+// math.hpp:26-37 (products of c[0..3], then the second term of each added);
+// rows 0-1 use the complex-product form B_TOP, rows 2-3 B_BOTTOM.
+template <bool B_TOP, bool B_BOTTOM>
+IDG_HD inline void jones_mul_f(const cfloat *a, const cfloat *b, cfloat *c) {
+  auto mt = [](cfloat x, cfloat y) { return B_TOP ? cmul_b(x, y) : cmul(x, y); };
+  auto mb = [](cfloat x, cfloat y) {
+    return B_BOTTOM ? cmul_b(x, y) : cmul(x, y);
+  };
+  c[0] = cadd(mt(a[0], b[0]), mt(a[1], b[2]));
+  c[1] = cadd(mt(a[0], b[1]), mt(a[1], b[3]));
+  c[2] = cadd(mb(a[2], b[0]), mb(a[3], b[2]));
+  c[3] = cadd(mb(a[2], b[1]), mb(a[3], b[3]));
+}
+
 IDG_HD inline void jones_mul(const cfloat *a, const cfloat *b, cfloat *c) {
-  c[0] = cadd(cmul(a[0], b[0]), cmul(a[1], b[2]));
-  c[1] = cadd(cmul(a[0], b[1]), cmul(a[1], b[3]));
-  c[2] = cadd(cmul(a[2], b[0]), cmul(a[3], b[2]));
-  c[3] = cadd(cmul(a[2], b[1]), cmul(a[3], b[3]));
+  jones_mul_f<false, false>(a, b, c);
 }
 
 IDG_HD inline void jones_hermitian(const cfloat *a, cfloat *h) {
@@ -67,22 +86,23 @@ IDG_HD inline void jones_hermitian(const cfloat *a, cfloat *h) {
   h[3] = cconj(a[3]);
 }
 
-// Gridder: pixels <- A1^H * pixels * A2
+// Gridder: pixels <- A1^H * pixels * A2, with the reference build's product
+// forms (A1^H P: rows 0-1 form a, rows 2-3 form b; (A1^H P) A2: form b).
 IDG_HD inline void apply_aterm_gridder(cfloat *pixels, const cfloat *a1,
                                        const cfloat *a2) {
   cfloat a1h[4], tmp[4];
   jones_hermitian(a1, a1h);
-  jones_mul(a1h, pixels, tmp);
-  jones_mul(tmp, a2, pixels);
+  jones_mul_f<false, true>(a1h, pixels, tmp);
+  jones_mul_f<true, true>(tmp, a2, pixels);
 }
 
-// Degridder: pixels <- A1 * pixels * A2^H
+// Degridder: pixels <- A1 * pixels * A2^H (A1 P: form a; (A1 P) A2^H: b).
 IDG_HD inline void apply_aterm_degridder(cfloat *pixels, const cfloat *a1,
                                          const cfloat *a2) {
   cfloat a2h[4], tmp[4];
-  jones_mul(a1, pixels, tmp);
+  jones_mul_f<false, false>(a1, pixels, tmp);
   jones_hermitian(a2, a2h);
-  jones_mul(tmp, a2h, pixels);
+  jones_mul_f<true, true>(tmp, a2h, pixels);
 }
 
 }  // namespace idg

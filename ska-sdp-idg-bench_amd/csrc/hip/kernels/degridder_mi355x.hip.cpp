@@ -845,12 +845,21 @@ DegridderSet degridder_set_for(bool nw8, bool tail) {
 // IDG_DEGRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
 static int degridder_impl() {
   const char *v = std::getenv("IDG_DEGRIDDER_IMPL");
+  if (v && std::string(v) == "sequential") return 2;
   return (v && std::string(v) == "valu") ? 0 : 1;
 }
 
 KernelChoice select_degridder(const Problem &p) {
   KernelChoice k;
   k.grid = p.nr_subgrids;
+  if (degridder_impl() == 2) {  // bit-exact to the reference's CPU output
+    k.func = sequential_degridder(p.subgrid_size);
+    k.block = sequential_block();
+    k.name = p.subgrid_size == 32   ? "degridder_sequential_mi355x_s32"
+             : p.subgrid_size == 64 ? "degridder_sequential_mi355x_s64"
+                                    : "degridder_sequential_mi355x_generic";
+    return k;
+  }
   k.block = kBlock;
   const int C = p.nr_channels;
   const bool cg8 = C % 8 == 0 || (C % 4 != 0 && C >= 8);

@@ -1243,15 +1243,26 @@ GridderSet gridder_set_for(int prec) {
 #define IDG_GRID_SPLIT 1
 #endif
 
-// IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons).
+// IDG_GRIDDER_IMPL=valu selects the VALU mirror path (A/B comparisons);
+// IDG_GRIDDER_IMPL=sequential the order-preserving kernel, bit-exact to the
+// reference's CPU output (sequential_mi355x.hip.cpp).
 static int gridder_impl() {
   const char *v = std::getenv("IDG_GRIDDER_IMPL");
+  if (v && std::string(v) == "sequential") return 2;
   return (v && std::string(v) == "valu") ? 0 : 1;
 }
 
 KernelChoice select_gridder(const Problem &p) {
   KernelChoice k;
   k.grid = p.nr_subgrids;
+  if (gridder_impl() == 2) {
+    k.func = sequential_gridder(p.subgrid_size);
+    k.block = sequential_block();
+    k.name = p.subgrid_size == 32   ? "gridder_sequential_mi355x_s32"
+             : p.subgrid_size == 64 ? "gridder_sequential_mi355x_s64"
+                                    : "gridder_sequential_mi355x_generic";
+    return k;  // no FFT epilogue: launch() runs launch_subgrid_fft after it
+  }
   const bool mfma = gridder_impl() == 1;
   k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
   k.prec = precision_for(Direction::kGridder, p);

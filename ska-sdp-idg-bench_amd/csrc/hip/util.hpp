@@ -191,6 +191,14 @@ int precision_for(Direction dir, const Problem &p);
 KernelChoice select_gridder(const Problem &p);
 KernelChoice select_degridder(const Problem &p);
 
+// The order-preserving kernels (kernels/sequential_mi355x.hip.cpp): the
+// reference CPU path's rounding sequence, bit for bit; 13-argument ABI, grid
+// = nr_subgrids, block = sequential_block().  Selected per call by
+// IDG_GRIDDER_IMPL=sequential / IDG_DEGRIDDER_IMPL=sequential.
+const void *sequential_gridder(int subgrid_size);
+const void *sequential_degridder(int subgrid_size);
+int sequential_block();
+
 // Returns an empty string if every subgrid's time range, stations and A-term
 // slot lie inside the buffers, else a description of the first violation.
 std::string validate(const Problem &p, const Extents &e,
