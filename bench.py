@@ -138,6 +138,11 @@ def parse(argv=None):
                     help="skip timing the FFT / adder / grid-sum / splitter")
     ap.add_argument("--no-weak", action="store_true",
                     help="skip the replicated (weak-scaling) side figure")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the side legs of a one-GPU default run (the "
+                         "wterm batch and the sequential kernels; profiling "
+                         "runs pass it so only the headline launches are "
+                         "counted)")
     ap.add_argument("--dump", default=None,
                     help="rank 0 writes the gathered gridder subgrids, "
                          "degridded visibilities and summed uv grid here "
@@ -500,6 +505,90 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled,
 
 
 # ---------------------------------------------------------------------------
+# Side legs of a one-GPU default run (beside `value`, never in it)
+# ---------------------------------------------------------------------------
+def time_side_legs(args, w, a, dev, nsub, stream, dist, value):
+    """Two figures the default line carries beside `value`:
+      wterm       the same batch with the 'wterm' workload's w-terms (w ~
+                  U(-200, 200), W_STEP = 2.5, 7 w-layers): every subgrid off
+                  the mirror pairing the synthetic w = 0 data allows
+                  (app/common/init.cpp:21), so `value` / this = the w = 0
+                  mirror factor; roofline priced from its own SQ profile;
+      sequential  the batch on the order-preserving kernels
+                  (IDG_{GRIDDER,DEGRIDDER}_IMPL=sequential), bit-exact to the
+                  reference's CPU output."""
+    import numpy as np
+    import torch
+    import idg_amd
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+    nvis = nsub * T * C
+    side = {}
+    steps = max(1, min(args.steps, 5))
+    # -- wterm: new uvw (w column) and metadata (w-layer), same visibilities
+    ww = workload("wterm")
+    aw = {"uvw": a["uvw"].copy(), "metadata": a["metadata"].copy()}
+    apply_wterms(ww, aw)
+    devw = dict(dev)
+    devw["uvw"] = torch.from_numpy(aw["uvw"]).cuda()
+    devw["metadata"] = torch.from_numpy(
+        aw["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
+    el, tg, td, _, _, _ = time_steps(ww, devw, nsub, steps, 1, stream, dist,
+                                     min_warmup_s=0.5)
+    flops = idg_amd.flops_gridder(C, nsub * T, nsub, S)
+    names = {d: idg_amd.kernel_name(d, S, C) for d in ("gridder", "degridder")}
+    dom = "gridder" if tg >= td else "degridder"
+    t_dom = max(tg, td)
+    entry = profile_entry(args.traffic_file, "wterm", names[dom])
+    rl = roofline_for(entry, names[dom], flops, nvis, t_dom, nsub,
+                      nsub if entry else 0, ww)
+    if entry and entry.get("algorithmic_bytes"):
+        rl["algorithmic_bytes"] = int(entry["algorithmic_bytes"])
+    wv = nvis / (el / steps) / 1e6
+    side["wterm"] = {
+        "value": round(wv, 2), "unit": "Mvis/s", "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 4),
+        "gridder_ms": round(tg * 1e3, 4), "degridder_ms": round(td * 1e3, 4),
+        "kernels": names, "roofline": rl,
+        "mirror_factor": round(value / wv, 3),
+        "workload": (f"the default batch with W_STEP={ww['w_step']}, "
+                     f"w~U(-{ww['w_range']:g},{ww['w_range']:g}), "
+                     f"w-layers={ww['w_layers']} (bench.py apply_wterms)"),
+        "note": "beside `value`, not in it: every subgrid on the general "
+                "(non-mirror) path; mirror_factor = value / this"}
+    del devw
+    # -- sequential kernels on the default batch
+    saved = {k: os.environ.get(k) for k in ("IDG_GRIDDER_IMPL",
+                                            "IDG_DEGRIDDER_IMPL")}
+    os.environ["IDG_GRIDDER_IMPL"] = "sequential"
+    os.environ["IDG_DEGRIDDER_IMPL"] = "sequential"
+    try:
+        names_q = {d: idg_amd.kernel_name(d, S, C)
+                   for d in ("gridder", "degridder")}
+        qsteps = max(1, min(args.steps, 2))
+        el, tg, td, _, _, _ = time_steps(w, dev, nsub, qsteps, 1, stream,
+                                         dist, min_warmup_s=0.0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    qv = nvis / (el / qsteps) / 1e6
+    side["sequential"] = {
+        "value": round(qv, 2), "unit": "Mvis/s", "steps": qsteps,
+        "ms_per_step": round(el / qsteps * 1e3, 4),
+        "gridder_ms": round(tg * 1e3, 4), "degridder_ms": round(td * 1e3, 4),
+        "gridder_mvis_s": round(nvis / tg / 1e6, 2),
+        "degridder_mvis_s": round(nvis / td / 1e6, 2),
+        "kernels": names_q, "slowdown_vs_value": round(value / qv, 2),
+        "note": "IDG_{GRIDDER,DEGRIDDER}_IMPL=sequential: the reference CPU "
+                "path's rounding sequence (glibc sincosf restated, t-then-c "
+                "f32 sums per pixel; y-then-x per visibility), bit-exact to "
+                "app/CPU (tests/test_gpu_sequential.py); beside `value`"}
+    return side
+
+
+# ---------------------------------------------------------------------------
 # Timed run
 # ---------------------------------------------------------------------------
 def dtype_label(kernels):
@@ -794,6 +883,7 @@ def plan_line(args, w, a, world, dist):
 
 
 def main(argv=None):
+    t_run0 = time.perf_counter()
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # a plain `python bench.py --gpus N`: become the launcher
@@ -956,6 +1046,14 @@ def main(argv=None):
                     "value = all ranks' visibilities / max over ranks",
         }
 
+    # ---- the wterm batch and the sequential kernels, beside `value` -------
+    side = None
+    if (world == 1 and args.workload == "default" and not args.no_side and
+            not args.dump):
+        progress("side legs (wterm batch, sequential kernels)")
+        side = time_side_legs(args, w, a, dev, nsub, stream, dist,
+                              nvis_job / sec_per_step / 1e6)
+
     sharded = args.mode == "sharded" and world > 1
     result = {
         "metric": METRIC,
@@ -1005,11 +1103,27 @@ def main(argv=None):
         "reference_hip_mi355x": (reference_hip_for(
             args.workload, sec_per_step, t_grid, t_degrid)
             if world == 1 else None),
+        "wterm": side["wterm"] if side else None,
+        "sequential": side["sequential"] if side else None,
         "cpu_baseline": None,
     }
+    t_cpu = 0.0
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         progress("cpu baseline")
+        t_c0 = time.perf_counter()
         result["cpu_baseline"] = cpu_baseline(w, a, args.cpu_sample_subgrids)
+        t_cpu = time.perf_counter() - t_c0
+    t_run = time.perf_counter() - t_run0
+    result["run_time_share"] = {
+        "run_s": round(t_run, 2),
+        "timed_region_s": round(elapsed, 4),
+        "cpu_baseline_s": round(t_cpu, 2),
+        "timed_frac": round(elapsed / t_run, 4),
+        "cpu_baseline_frac": round(t_cpu / t_run, 4),
+        "note": "wall time of this process (from argument parsing): the timed "
+                "steps behind `value` are timed_region_s of it; the rest is "
+                "batch generation, upload, warm-up, side legs and the CPU "
+                "baseline"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()

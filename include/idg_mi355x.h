@@ -251,6 +251,19 @@ int idg_generate(int nr_stations, int nr_timeslots, int nr_timesteps,
                  idg_cfloat_t *aterms, idg_metadata_t *metadata,
                  idg_cfloat_t *subgrids, int nthreads);
 
+/* ---- workspaces -----------------------------------------------------------
+ * The device entries keep their scratch (the two-kernel form's subgrid queue,
+ * the adder's home sort and segment lists) cached per (device, stream), so a
+ * launch makes no allocation.  idg_release_workspaces frees the cache of
+ * `stream` on the current device (all != 0: of every stream of the current
+ * device).  The stream(s) must be idle (their work complete): call it before
+ * destroying a stream the entries used -- a new stream may be given the same
+ * handle -- and before hipDeviceReset.  Returns IDG_OK or a HIP error code
+ * (hipErrorNotReady: a slot was being enqueued on by another host thread and
+ * was left).  No reference counterpart (the reference allocates per call,
+ * app/HIP/util.cpp:220-232). */
+int idg_release_workspaces(void *stream, int all);
+
 const char *idg_last_error(void);
 
 #ifdef __cplusplus

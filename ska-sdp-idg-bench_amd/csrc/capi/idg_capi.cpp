@@ -99,6 +99,12 @@ int idg_abi_version(void) { return IDG_MI355X_ABI_VERSION; }
 
 const char *idg_last_error(void) { return g_last_error.c_str(); }
 
+int idg_release_workspaces(void *stream, int all) {
+  return from_hip(idg_mi355x::release_workspaces(
+                      static_cast<hipStream_t>(stream), all != 0),
+                  "idg_release_workspaces");
+}
+
 int idg_subgrid_fft_launch(int nr_subgrids, int subgrid_size, int sign,
                            float scale, idg_cfloat_t *subgrids, void *stream) {
   if (nr_subgrids < 0 || subgrid_size <= 0 || subgrid_size > 64 ||

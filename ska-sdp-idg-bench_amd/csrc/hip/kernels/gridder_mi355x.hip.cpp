@@ -1265,7 +1265,14 @@ KernelChoice select_gridder(const Problem &p) {
   }
   const bool mfma = gridder_impl() == 1;
   k.block = mfma ? 64 * IDG_GRID_NW : kBlock;
+  // the options the selected kernel is built with (reported by
+  // idg_precision_options / bench.py): the alternating tail replaces the
+  // every-phasor one, blocked summation exists at S = 32 only, and the VALU
+  // kernel has none of them
   k.prec = precision_for(Direction::kGridder, p);
+  if (k.prec & kPrecTailAlt) k.prec &= ~kPrecTail;
+  if (p.subgrid_size != 32) k.prec &= ~kPrecFlush;
+  if (!mfma) k.prec = 0;
   // the FFT in the gridder's epilogue (S = 32, MFMA; IDG_GRID_FFT=0: the
   // launch layer runs launch_subgrid_fft after the plain gridder instead)
   const char *fenv = std::getenv("IDG_GRID_FFT");

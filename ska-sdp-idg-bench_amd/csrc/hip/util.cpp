@@ -237,7 +237,10 @@ int precision_for(Direction dir, const Problem &p) {
   // over channels; measured 1.00e-6 vs 0.97e-6 from exact at the -c
   // defaults, 8.1e-7 vs 6.7e-7 at C = 256, for 5 % of its time)
   if (dir == Direction::kDegridder) return 0;
-  return kPrecTailAlt | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
+  // the one-channel-per-quad tail cancels only over whole channel quads:
+  // with a partial last quad the every-phasor tail instead
+  const int tail = p.nr_channels % 4 == 0 ? kPrecTailAlt : kPrecTail;
+  return tail | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
 }
 
 std::string validate(const Problem &p, const Extents &e,
@@ -396,6 +399,40 @@ WorkspaceLease::~WorkspaceLease() {
   WorkspaceSlot &w = g_ws[std::make_tuple(dev_, stream, slot_)];
   w.busy = false;
   w.clean = leave_clean;
+}
+
+hipError_t release_workspaces(hipStream_t stream, bool all) {
+  int dev = 0;
+  hipError_t err = hipGetDevice(&dev);
+  if (err != hipSuccess) return err;
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  bool freed = false, busy = false;
+  for (auto it = g_ws.begin(); it != g_ws.end();) {
+    if (std::get<0>(it->first) != dev ||
+        (!all && std::get<1>(it->first) != stream)) {
+      ++it;
+      continue;
+    }
+    if (it->second.busy) {
+      busy = true;
+      ++it;
+      continue;
+    }
+    // freed on the null stream (the owning stream may be about to go), then
+    // waited for, so the memory is gone when this returns
+    if (it->second.ptr) {
+      const hipError_t e = hipFreeAsync(it->second.ptr, nullptr);
+      if (e != hipSuccess && err == hipSuccess) err = e;
+      freed = true;
+    }
+    it = g_ws.erase(it);
+  }
+  if (freed) {
+    const hipError_t e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess && err == hipSuccess) err = e;
+  }
+  if (err == hipSuccess && busy) err = hipErrorNotReady;
+  return err;
 }
 
 hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,

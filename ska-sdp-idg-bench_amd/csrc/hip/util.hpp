@@ -154,11 +154,15 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
 // (never clean) freed after the sequence.
 constexpr int kWorkspaceQueue = 0, kWorkspaceHomeSort = 1,
               kWorkspaceAdderSeg = 2;
+// Not copyable: a copy would release the slot twice.
 struct WorkspaceLease {
   void *ptr = nullptr;
   hipStream_t stream = nullptr;
   bool clean = false;
   bool leave_clean = false;
+  WorkspaceLease() = default;
+  WorkspaceLease(const WorkspaceLease &) = delete;
+  WorkspaceLease &operator=(const WorkspaceLease &) = delete;
   hipError_t acquire(hipStream_t s, int slot, size_t bytes);
   ~WorkspaceLease();
 
@@ -166,6 +170,14 @@ struct WorkspaceLease {
   int dev_ = 0, slot_ = 0;
   bool private_ = false;
 };
+
+// Frees the cached workspaces of `stream` on the current device (all = true:
+// of every stream of the current device).  The stream(s) must be idle: call
+// it before destroying a stream the entries have used (a new stream may get
+// the same handle) and before hipDeviceReset.  A slot leased at the moment
+// (another host thread enqueueing on it) is left alone and reported as
+// hipErrorNotReady.  idg_release_workspaces in the C ABI.
+hipError_t release_workspaces(hipStream_t stream, bool all);
 
 // Whether the device entries launch the two-kernel form (mirror kernel +
 // queue-fed general kernel) or the one combined kernel: the two-kernel form

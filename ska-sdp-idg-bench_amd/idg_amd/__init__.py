@@ -12,6 +12,7 @@ from .api import (IMAGE_SIZE, METADATA_DTYPE, NR_CORRELATIONS, W_STEP,
                   host_chunk_plan,
                   kernel_name,
                   nr_subgrids_for, precision_options, p_run_degridder, p_run_gridder,
+                  release_workspaces,
                   splitter_fft_launch, splitter_launch, subgrid_fft_launch,
                   validate_metadata)
 from ._lib import LIB_PATH
@@ -23,7 +24,7 @@ __all__ = [
     "c_run_degridder", "c_run_gridder", "degrid_from", "degridder_launch",
     "device_name", "flops_gridder", "generate", "grid_onto",
     "gridder_fft_launch", "gridder_launch", "host_chunk_plan", "kernel_name", "nr_subgrids_for", "p_run_degridder",
-    "precision_options",
+    "precision_options", "release_workspaces",
     "p_run_gridder", "splitter_fft_launch", "splitter_launch",
     "subgrid_fft_launch",
     "validate_metadata", "LIB_PATH", "shard",

@@ -52,6 +52,7 @@ SIGNATURES = {
     "idg_adder_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
     "idg_splitter_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
     "idg_splitter_fft_launch": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "idg_release_workspaces": (_I, [_P, _I]),
 }
 
 

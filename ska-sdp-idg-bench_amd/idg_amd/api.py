@@ -490,3 +490,19 @@ def bytes_gridder(nr_channels, nr_timesteps, nr_subgrids, subgrid_size,
 
 def abi_version():
     return lib.idg_abi_version()
+
+
+def release_workspaces(stream=None, all_streams=False):
+    """Free the device workspaces the launch entries cache for `stream` (a
+    torch stream; None = the current stream) on the current device, or for
+    every stream with all_streams=True (include/idg_mi355x.h
+    idg_release_workspaces).  The stream must be idle: call it before
+    dropping a stream the entries have used."""
+    import torch
+    if all_streams:
+        handle = ctypes.c_void_p(None)
+    else:
+        handle = _stream_handle(stream)
+        (stream or torch.cuda.current_stream()).synchronize()
+    _check(lib.idg_release_workspaces(handle, 1 if all_streams else 0),
+           "idg_release_workspaces")

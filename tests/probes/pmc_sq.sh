@@ -14,7 +14,7 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || { echo "pass $i failed"; exit 1; }
+    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline --no-side > /dev/null 2> "$out/p$i.err" || { echo "pass $i failed"; exit 1; }
 done
 # optional: the VALU instruction classes (for the issue model's prices);
 # a counter this rocprofv3 does not know ends only this pass
@@ -25,6 +25,6 @@ for grp in "SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INS
   for c in $grp; do grep -qw "$c" "$out/avail.txt" || miss="$miss $c"; done
   [ -n "$miss" ] && { echo "pass $i skipped (not listed:$miss)"; continue; }
   timeout -s KILL 120 rocprofv3 --pmc $grp -d "$out/p$i" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline > /dev/null 2> "$out/p$i.err" || echo "optional pass $i failed"
+    python3 "$GRAFT_REPO_ROOT/bench.py" ${BENCH_ARGS:-} --steps 1 --warmup 1 --min-warmup-s 0 --no-cpu-baseline --no-side > /dev/null 2> "$out/p$i.err" || echo "optional pass $i failed"
 done
 echo done

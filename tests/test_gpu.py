@@ -547,7 +547,9 @@ def test_large_configs_sampled_subgrids_vs_oracle(idg, oracle_lib, cfg):
 
 
 @pytest.mark.timeout(900)
-def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib):
+@pytest.mark.parametrize("impl", ["mfma", "sequential"])
+def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib,
+                                                          impl, monkeypatch):
     """BASELINE configs[2] at full size: C = 256, NR_TIMESLOTS = 20, 24,500
     subgrids, 3.2e9 complex visibilities (25.7 GB) resident on the device.
     The reference's int sizes and indices overflow here
@@ -559,8 +561,16 @@ def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib):
     is held to 1e-5 in the scale-free normalised RMS (at
     T x C = 32,768 the reference metric grows with sqrt of the pixel
     magnitude) and the reference metric is printed beside it; the
-    degridder to the reference metric."""
+    degridder to the reference metric.  impl="sequential" (the
+    order-preserving kernels): every sampled output bit-exact to the oracle
+    (itself bit-exact to app/CPU) and, where oracle/_ref is built, the
+    reference metric against the reference's own CPU output <= 1e-5 (it is
+    0)."""
     import torch
+    import oracle as orc
+    if impl == "sequential":
+        monkeypatch.setenv("IDG_GRIDDER_IMPL", "sequential")
+        monkeypatch.setenv("IDG_DEGRIDDER_IMPL", "sequential")
     st, ts, T, C, G, S = 50, 20, 128, 256, 1024, 32
     a = idg.generate(st, ts, T, C, G, S, nthreads=16)
     ns = idg.nr_subgrids_for(st, ts)
@@ -577,8 +587,11 @@ def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib):
         g_dev = _dgrid(idg, p, dev, dev["visibilities"])
         d_dev = _ddegrid(idg, p, dev, dev["subgrids"])
         torch.cuda.synchronize()
-        sample_split(idg, oracle_lib, p, a, samples,
-                     g_dev[list(samples)].cpu().numpy(), "full_configs2")
+        if impl == "mfma":
+            sample_split(idg, oracle_lib, p, a, samples,
+                         g_dev[list(samples)].cpu().numpy(), "full_configs2")
+        ref = orc.Reference(portable=True) \
+            if orc.Reference.available(portable=True) else None
         q = dict(p, nr_subgrids=1)
         for s in samples:
             md0 = a["metadata"][s:s + 1].copy()
@@ -597,12 +610,23 @@ def test_full_configs2_batch_past_int32_offsets_vs_oracle(idg, oracle_lib):
                                  np.ascontiguousarray(a["subgrids"][s:s + 1]))
             d = d_dev[s:s + 1].cpu().numpy()
             derr = oracle_lib.check_error(d, do)[0]
-            print(f"configs[2] subgrid {s} (vis offset "
+            print(f"configs[2] {impl} subgrid {s} (vis offset "
                   f"{int(a['metadata']['time_offset'][s]) * C * 4} complex): "
                   f"gridder rel-RMS {rel:.3e} reference-metric "
                   f"{ref_metric:.3e}; degridder reference-metric {derr:.3e}")
             assert rel <= TOLERANCE, s
             assert derr <= TOLERANCE, s
+            if impl == "sequential":
+                assert np.array_equal(g.view(np.uint32), go.view(np.uint32)), s
+                assert np.array_equal(d.view(np.uint32), do.view(np.uint32)), s
+                if ref is not None:
+                    gr = np.zeros_like(go)
+                    ref.gridder(*_params(q), uvw, a["wavenumbers"],
+                                np.ascontiguousarray(a["visibilities"][s]),
+                                a["spheroidal"], a["aterms"], md0, gr)
+                    e_ref = oracle_lib.check_error(g, gr)[0]
+                    print(f"  vs app/CPU (oracle/_ref): {e_ref:.3e}")
+                    assert e_ref <= TOLERANCE, s
     finally:
         del dev
         torch.cuda.empty_cache()
@@ -897,6 +921,35 @@ def test_queue_workspace_reused_across_launches(idg, full_mixed, op,
     torch.cuda.synchronize()
     for out in again:
         assert torch.equal(out, first)
+
+
+def test_workspaces_released_with_their_stream(idg, full_mixed,
+                                               monkeypatch):
+    """idg_release_workspaces: the split-form launches on a private stream
+    cache their queue for it; releasing that stream's workspaces (the stream
+    idle) and dropping the stream, then launching on fresh streams -- which
+    may get the same handle -- and releasing every stream's, all give the
+    default stream's output bit for bit."""
+    import torch
+    p, a, dev = full_mixed
+    monkeypatch.setenv("IDG_KERNEL_FORM", "split")
+    want = _dgrid(idg, p, dev, dev["visibilities"])
+    torch.cuda.synchronize()
+    for i in range(3):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            out = torch.empty_like(want)
+            idg.gridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                               dev["visibilities"], dev["spheroidal"],
+                               dev["aterms"], dev["metadata"], out, stream=st)
+        st.synchronize()
+        assert torch.equal(out, want), i
+        idg.release_workspaces(st)
+        del st
+    idg.release_workspaces(all_streams=True)
+    again = _dgrid(idg, p, dev, dev["visibilities"])
+    torch.cuda.synchronize()
+    assert torch.equal(again, want)
 
 
 @pytest.mark.parametrize("form", ["combined", "split"])

@@ -176,6 +176,47 @@ def test_adder_crowded_tiles_split_into_segments(idg, S, G, ns, sigma,
     assert _rel(got, serial) < 1e-5
 
 
+@pytest.mark.parametrize("W", [2, 3])
+def test_adder_crowded_tiles_in_several_w_layers(idg, W, monkeypatch):
+    """The segmented adder with crowded tiles in more than one w-layer: the
+    segment lists are indexed per (layer, tile), only the first row of
+    segment workgroups sums them, and the combine offsets the grid by the
+    layer.  Each layer gets its own centre-concentrated crowd (> 256
+    overlapping subgrids on its densest tile): numpy, bit-reproducible, and
+    the one-workgroup-per-tile form (IDG_ADD_SEG=0) agree."""
+    import torch
+    S, G, per = 32, 256, 1500
+    rng = np.random.default_rng(100 + W)
+    ns = per * W
+    md = np.zeros(ns, METADATA_DTYPE)
+    c = (G - S) / 2
+    md["x"] = np.clip(np.rint(rng.normal(c, 12.0, ns)), 0, G - S)
+    md["y"] = np.clip(np.rint(rng.normal(c, 12.0, ns)), 0, G - S)
+    md["z"] = np.repeat(np.arange(W), per)
+    rng.shuffle(md["z"])
+    for z in range(W):
+        assert _tile_overlaps(md[md["z"] == z], G, S).max() > 256, z
+    sub = rng.normal(size=(ns, 4, S, S)) + 1j * rng.normal(size=(ns, 4, S, S))
+    t_sub = torch.from_numpy(pl.to_pairs(sub)).cuda()
+    t_md = _md_tensor(md)
+
+    def run():
+        grid = torch.zeros((W, 4, G, G, 2), dtype=torch.float32, device="cuda")
+        idg.adder_launch(G, t_md, t_sub, grid, W)
+        torch.cuda.synchronize()
+        return grid
+
+    grids = [run(), run()]
+    assert torch.equal(grids[0], grids[1])
+    got = pl.to_complex(grids[0].cpu().numpy())
+    ref = pl.adder(np.zeros((W, 4, G, G), complex), md,
+                   pl.to_complex(pl.to_pairs(sub)))
+    assert _rel(got, ref) < 1e-5
+    monkeypatch.setenv("IDG_ADD_SEG", "0")
+    serial = pl.to_complex(run().cpu().numpy())
+    assert _rel(got, serial) < 1e-5
+
+
 @pytest.mark.parametrize("S,G,W", [(32, 128, 1), (16, 96, 3)])
 def test_adder_uncrowded_tiles_bitwise_the_one_workgroup_form(idg, S, G, W,
                                                               monkeypatch):

@@ -169,6 +169,22 @@ def test_precision_options_defaults_and_override(monkeypatch):
     bits, desc = idg_amd.precision_options("gridder", 32, 256)
     assert bits == 6 and "blocked summation" in desc
     assert idg_amd.precision_options("degridder", 32, 256) == (0, "none")
+    # what is built: no blocked summation off S = 32 ...
+    assert idg_amd.precision_options("gridder", 64, 256)[0] == 4
+    # ... the every-phasor tail where the channels end in a partial quad ...
+    assert idg_amd.precision_options("gridder", 32, 15)[0] == 1
+    assert idg_amd.precision_options("gridder", 32, 300)[0] == 6
+    assert idg_amd.precision_options("gridder", 32, 301)[0] == 3
+    # ... and the alternating tail alone when both tails are asked for
+    monkeypatch.setenv("IDG_PREC", "5")
+    assert idg_amd.precision_options("gridder", 32, 16)[0] == 4
+    monkeypatch.setenv("IDG_GRIDDER_IMPL", "valu")
+    assert idg_amd.precision_options("gridder", 32, 16)[0] == 0
+    monkeypatch.setenv("IDG_GRIDDER_IMPL", "sequential")
+    assert idg_amd.precision_options("gridder", 32, 16)[0] == 0
+    assert idg_amd.kernel_name("gridder", 32, 16) == \
+        "gridder_sequential_mi355x_s32"
+    monkeypatch.delenv("IDG_GRIDDER_IMPL")
     monkeypatch.setenv("IDG_PREC", "1")
     assert idg_amd.precision_options("gridder", 32, 16)[0] == 1
     assert idg_amd.precision_options("degridder", 64, 16)[0] == 1
