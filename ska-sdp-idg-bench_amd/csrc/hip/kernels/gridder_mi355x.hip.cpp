@@ -1169,6 +1169,11 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
   const int tid = threadIdx.x;
   const QueueView qv = queue_view(queue, nr_subgrids);
   const int count = all ? nr_subgrids : qv.count();
+  // An empty queue (every subgrid took the mirror path: the benchmark data)
+  // leaves every counter at zero, so no workgroup takes a position or
+  // retires: all return before any atomic (the resident grid's serialized
+  // take and exit atomics were most of this launch's 15 us).
+  if (count == 0) return;
   // the next queue position, taken by thread 0 and passed on through lds[0]
   // (between subgrids, where grid_mfma uses no LDS)
   if (tid == 0)
