@@ -1160,7 +1160,7 @@ def dump_outputs(path, a, part, outs, grid_sum, rank, world, mode, dist):
 
 def reference_hip_for(workload_name, sec_per_step, t_grid, t_degrid):
     """The reference's own HIP kernels measured on MI355X at configs[1]
-    (profiles/reference_hip.json, made by tests/debug/ref_hip.sh): this
+    (profiles/reference_hip.json, made by tools/debug/ref_hip.sh): this
     run's per-GPU rates over theirs, for the fastest reference kernels and
     for the fastest that pass the reference's own -c check."""
     if workload_name != "default":

@@ -947,7 +947,7 @@ void c_run_degridder(
 
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
 // Debug builds only: the last combined-degridder launch's workgroup stamps
-// (tests/debug/wg_timeline.py).
+// (tools/debug/wg_timeline.py).
 extern "C" int idg_debug_timeline_degridder_copy(void *host, int n) {
   return hipMemcpyFromSymbol(
       host, HIP_SYMBOL(idg_mi355x::idg_debug_timeline_degridder),

@@ -71,7 +71,7 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
 // channel of every channel quad and nothing to the other three -- the same
 // correction summed over each quad, for a quarter of the adds: the gridder
 // sums over channels, so the +3c / -c pattern cancels in every coherent sum
-// to first order (tests/debug/tail_mean_emul.py); kPrecFlush
+// to first order (tests/emul/tail_mean_emul.py); kPrecFlush
 // (gridder, S = 32) sums the accumulator tiles into an f32 master every
 // kFlushFills fills (at most 32 K-steps each).
 constexpr int kPrecTail = 1, kPrecFlush = 2, kPrecTailAlt = 4;
@@ -92,7 +92,7 @@ __device__ __forceinline__ void phase_tail(float phase_offset, float *c,
 // The value of lane (l + 8) mod 16 of the lane's 16-lane row (DPP
 // row_ror:8).  Call it on a named scalar: applied to the elements of an
 // ext_vector in a loop, this hipcc emitted one DPP move of element 0 for
-// all of them (tests/probes/dpp_vector_probe.hip).
+// all of them (tools/probes/dpp_vector_probe.hip).
 __device__ __forceinline__ float row_ror8(float x) {
   return __builtin_bit_cast(
       float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128,
@@ -111,7 +111,7 @@ __device__ __forceinline__ void rotate4(float (&v)[8], float c, float s) {
 
 // sin / cos of 2*pi*r for r in revolutions.  v_sin_f32 / v_cos_f32 take
 // their argument in revolutions and are exact enough once r is small
-// (measured on MI355X: tests/probes); the range
+// (measured on MI355X: tools/probes); the range
 // reduction is done by revolutions() / the anchored update in the kernels,
 // never by the hardware's own [-256, 256] fold of a large, already-rounded
 // argument (the trap of __sinf/__cosf).
@@ -275,7 +275,7 @@ __device__ __forceinline__ void load_jones(const float4 *p, idg::cfloat *j) {
 
 }  // namespace idg_mi355x
 
-// Debug builds only (-DIDG_WG_TIMELINE=1, tests/debug/wg_timeline.py): per
+// Debug builds only (-DIDG_WG_TIMELINE=1, tools/debug/wg_timeline.py): per
 // workgroup wall-clock start / end (s_memrealtime, 100 MHz), HW_ID and
 // XCC_ID of the combined kernels, written by thread 0 with vector stores.
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE

@@ -281,7 +281,7 @@ constexpr int general_lds_words() {
 // ignored), so the asm saves and restores it around its own use; and the
 // SALU write of M0 is followed by one wait state before the LDS-DMA reads
 // it (the gfx9 "M0 write -> LDS DMA" hazard, which the compiler cannot pad
-// inside an asm string; tests/probes/dma_drain_check.py checks the listing).
+// inside an asm string; tools/probes/dma_drain_check.py checks the listing).
 __device__ __forceinline__ void l2_prefetch_dma(const void *src,
                                                 const void *lds_dst) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(
@@ -456,7 +456,7 @@ __device__ __forceinline__ void grid_mfma(
     };
     // (the four elements are taken into named scalars before their DPP
     // moves: written as a loop over a[r], this hipcc moved a[0] four times;
-    // tests/probes/dpp_vector_probe.hip)
+    // tools/probes/dpp_vector_probe.hip)
     auto flush_tile = [&](floatx4 &a, int t, float unsc) {
       const float a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
       const float v0 = (a0 + row_ror8(a0)) * unsc;
@@ -765,7 +765,7 @@ __device__ __forceinline__ void grid_mfma(
               // scheduler sank all of an iteration's MFMAs to the end of the
               // loop body, the last tile's accumulators came out corrupted
               // (a few % of subgrids, run-to-run different, only with >1
-              // wave per SIMD; DESIGN.md §4.4, tests/debug/diff_detail.py).
+              // wave per SIMD; DESIGN.md §4.4, tools/debug/diff_detail.py).
               IDG_KSTEP_FENCE();
             }
           }
@@ -1353,7 +1353,7 @@ void c_run_gridder(
 
 #if defined(IDG_WG_TIMELINE) && IDG_WG_TIMELINE
 // Debug builds only: the last combined-gridder launch's workgroup stamps
-// (tests/debug/wg_timeline.py).
+// (tools/debug/wg_timeline.py).
 extern "C" int idg_debug_timeline_gridder_copy(void *host, int n) {
   return hipMemcpyFromSymbol(
       host, HIP_SYMBOL(idg_mi355x::idg_debug_timeline_gridder),

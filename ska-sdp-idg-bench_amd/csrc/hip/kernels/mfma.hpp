@@ -8,7 +8,7 @@
 //   a = a_hi + a_lo   (a_hi = f16(a), a_lo = f16(a - a_hi), |err| ~ 2^-22|a|)
 //   A' = [a_hi, a_lo] stacked along K, B' = [b; b] repeated along K,
 //   B columns = [b_hi (8) | b_lo (8)], O = O[:, 0:8] + O[:, 8:16].
-// (measured: tests/probes/mfma_probe.hip)
+// (measured: tools/probes/mfma_probe.hip)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -103,7 +103,7 @@ __device__ __forceinline__ unsigned split_lo(float a, float b) {
 // one v_cvt_pk_f16_f32 per pair, i.e. f16(x - hi) with the same single
 // rounding as a v_fma_mix{lo,hi}_f16: bit for bit the same operand, but the
 // f16-output mix issues at half rate on gfx950 (8.5 vs 4.5 cycles,
-// tests/probes/instr_rates_probe.hip), so 8 mix_f32 + 4 cvt_pk cost 13
+// tools/probes/instr_rates_probe.hip), so 8 mix_f32 + 4 cvt_pk cost 13
 // cycles less per call than 8 mixlo/hi (split_rates_probe.hip).
 // Pads: `s_nop 0` first (the inputs are usually fresh v_sin/v_cos results:
 // trans -> VALU forwarding needs 1 state) and `s_nop 1` last (VALU write ->

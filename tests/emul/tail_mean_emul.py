@@ -15,7 +15,7 @@ double) against exact accumulation of the reference's f32 phases.
             over the block, 1/N of the adds
   altN      the same per channel: N x c on channels k % N == 0
 
-    python tests/debug/tail_mean_emul.py [C] [T]
+    python tests/emul/tail_mean_emul.py [C] [T]
 DESIGN.md §3.3.
 """
 import os
@@ -24,7 +24,7 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests/debug"):
+for _p in ("ska-sdp-idg-bench_amd", "oracle", "tools/debug"):
     sys.path.insert(0, os.path.join(REPO, _p))
 import idg_amd  # noqa: E402
 import oracle as orc  # noqa: E402

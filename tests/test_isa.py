@@ -2,7 +2,7 @@
 cross-compiles the listing with the library's own flags, `make isa`).
 
 * Wait states around the inline-asm f16 splits that feed the MFMAs
-  (tests/probes/hazard_check.py): every v_mfma SrcA/SrcB
+  (tools/probes/hazard_check.py): every v_mfma SrcA/SrcB
   written by a VALU has >= 2 wait states before it, every VALU read of a
   v_sin/v_cos result >= 1, on every control-flow path.
 * Register spills stay out of the MFMA loops: no scratch access inside any
@@ -18,7 +18,7 @@ import pytest
 
 from conftest import PKG, REPO
 
-sys.path.insert(0, os.path.join(REPO, "tests", "probes"))
+sys.path.insert(0, os.path.join(REPO, "tools", "probes"))
 import hazard_check as hc  # noqa: E402
 
 ISA = os.path.join(PKG, "build", "isa")
@@ -158,12 +158,12 @@ def test_dpp_moves_of_vector_elements(tmp_path):
     # hipcc (ROCm 7.2) emits one DPP move of element 0 for a loop of
     # update_dpp over a float4's elements written inline (loop_form); the
     # kernels go through device.hpp row_ror8 on named scalars (scalar_form),
-    # which must stay four moves (tests/probes/dpp_vector_probe.hip).
+    # which must stay four moves (tools/probes/dpp_vector_probe.hip).
     out = tmp_path / "dpp.s"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
                     "-ffp-contract=off", "-I", os.path.join(PKG, "csrc"),
                     "--cuda-device-only", "-S", "-o", str(out),
-                    os.path.join(REPO, "tests", "probes",
+                    os.path.join(REPO, "tools", "probes",
                                  "dpp_vector_probe.hip")],
                    check=True, capture_output=True, timeout=300)
     text = out.read_text()

@@ -6,7 +6,7 @@ ours_vs_exact / ref_vs_exact in the reference metric, plus the error of the
 largest pixels split into a coherent amplitude part (mean Re((o-e) e*)/|e|^2),
 a coherent phase part (the Im of the same) and the rest.  DESIGN.md §3.1.
 
-    python tests/debug/accuracy_ab.py [tag]
+    python tools/debug/accuracy_ab.py [tag]
 """
 import json
 import os

@@ -6,7 +6,7 @@ width, so the densest tile's overlap count crosses the LDS list's cap
 the metadata).  Prints, per layout, the densest tile's overlap count, the
 tiles over the cap and the adder's mean time (HIP events, 10 launches).
 
-    python tests/debug/adder_crowded.py [--sigmas 200,100,75,60,40,15]
+    python tools/debug/adder_crowded.py [--sigmas 200,100,75,60,40,15]
 """
 import argparse
 import json

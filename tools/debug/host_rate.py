@@ -2,7 +2,7 @@
 idg_c_run_degridder: allocate, copy in, launch, copy out, free -- the
 reference's c_run_* contract, app/HIP/util.cpp:255-311) at BASELINE
 configs[1], beside the resident-data kernel time.  Prints one JSON line.
-  python tests/debug/host_rate.py [--reps 3]"""
+  python tools/debug/host_rate.py [--reps 3]"""
 import argparse
 import json
 import os

@@ -1,5 +1,5 @@
 """Median / min duration of the pipeline kernels in rocprofv3 kernel-trace
-databases: python tests/debug/kt_pipeline.py gpurun_out/kt_*/run_results.db"""
+databases: python tools/debug/kt_pipeline.py gpurun_out/kt_*/run_results.db"""
 import collections
 import sqlite3
 import sys

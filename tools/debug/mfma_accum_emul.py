@@ -14,7 +14,7 @@ Each model changes one ingredient, so the error budget can be read off:
   flushN    rne, but the accumulator is added to an f32 master and cleared
             every N K-steps (blocked summation)
 
-    python tests/debug/mfma_accum_emul.py [C] [subgrid]
+    python tools/debug/mfma_accum_emul.py [C] [subgrid]
 DESIGN.md §3.1.
 """
 import os
@@ -23,7 +23,7 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests", "tests/debug"):
+for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests", "tools/debug"):
     sys.path.insert(0, os.path.join(REPO, _p))
 import idg_amd  # noqa: E402
 import oracle as orc  # noqa: E402

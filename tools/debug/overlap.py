@@ -5,7 +5,7 @@ two directions read and write disjoint buffers).  Wall clock of the K steps
 after >= 1 s of warm-up in the same form; full batch and the N = 2/4/8 shard
 sizes (first n subgrids).
 
-    python tests/debug/overlap.py [--steps 20] [--counts 24500,6125,3063]
+    python tools/debug/overlap.py [--steps 20] [--counts 24500,6125,3063]
 """
 import argparse
 import json

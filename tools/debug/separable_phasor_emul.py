@@ -8,7 +8,7 @@ compares, within one numpy emulation (both sums in double, the reference's
 own f32 phase_offset kept), the exact-math sum against the sum of the
 reference's f32 phases in the reference metric:
 
-    python tests/debug/separable_phasor_emul.py [C]
+    python tools/debug/separable_phasor_emul.py [C]
 
 Measured: 1.7e-5 at C = 16, 4.5e-5 at C = 256 -- above the 1e-5 bar, so the
 phase must keep the reference's rounding.  (The absolute
@@ -18,7 +18,7 @@ meaningful.)"""
 import os, sys
 import numpy as np
 REPO=os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-for p in ("ska-sdp-idg-bench_amd","oracle","tests","tests/debug"):
+for p in ("ska-sdp-idg-bench_amd","oracle","tests","tools/debug"):
     sys.path.insert(0, os.path.join(REPO,p))
 import idg_amd, oracle as orc
 from mfma_accum_emul import f32, f64, fma32

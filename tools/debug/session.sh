@@ -3,7 +3,7 @@
 # of rounds 2-3).  Every step runs under its own time limit, the steps are
 # chained, and the first failure ends the call.
 #
-#   bash tests/debug/session.sh OUTDIR STEP [STEP ...]
+#   bash tools/debug/session.sh OUTDIR STEP [STEP ...]
 #
 # STEP:
 #   suite[=K]            GPU test suite (pytest -m gpu), optional -k filter K
@@ -18,10 +18,10 @@
 #                        bench workload (profile_round.sh, pmc_sq.sh)
 #   accuracy[@LIB]       gridder distance to exact accumulation
 #                        (accuracy_ab.py)
-#   probe=NAME           a built probe executable (tests/probes/NAME)
+#   probe=NAME           a built probe executable (tools/probes/NAME)
 #
 # Example (the round-3 "lean splitter" A/B):
-#   bash tests/debug/session.sh gpurun_out/x 'suite@ab/lean.so=splitter' \
+#   bash tools/debug/session.sh gpurun_out/x 'suite@ab/lean.so=splitter' \
 #        abpipe=ab/lean.so,ab/shipped.so
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -56,26 +56,26 @@ for step in "$@"; do
 import json; d = json.load(open('$log')); k = d['kernels']
 print(d['value'], k['gridder']['ms'], k['degridder']['ms'])" ;;
     ab)
-      timeout -k 10 1200 bash tests/debug/ab.sh ${arg//,/ } > "$log" 2>&1
+      timeout -k 10 1200 bash tools/debug/ab.sh ${arg//,/ } > "$log" 2>&1
       rc=$?; cat "$log" ;;
     abpipe)
-      timeout -k 10 1200 bash tests/debug/ab_pipe.sh ${arg//,/ } > "$log" 2>&1
+      timeout -k 10 1200 bash tools/debug/ab_pipe.sh ${arg//,/ } > "$log" 2>&1
       rc=$?; cat "$log" ;;
     shard)
-      timeout -k 10 600 python -u tests/debug/shard_rate.py --steps 10 > "$log" 2>&1
+      timeout -k 10 600 python -u tools/debug/shard_rate.py --steps 10 > "$log" 2>&1
       rc=$?; grep predicted "$log" ;;
     profile)
       tag=${arg%%,*}
       bargs=""
       [ "$tag" != "$arg" ] && bargs=${arg#*,}
-      BENCH_ARGS="${bargs//,/ }" timeout -k 10 900 bash tests/probes/profile_round.sh "$tag" > "$log" 2>&1 &&
-      BENCH_ARGS="${bargs//,/ }" timeout -k 10 900 bash tests/probes/pmc_sq.sh "$tag" >> "$log" 2>&1
+      BENCH_ARGS="${bargs//,/ }" timeout -k 10 900 bash tools/probes/profile_round.sh "$tag" > "$log" 2>&1 &&
+      BENCH_ARGS="${bargs//,/ }" timeout -k 10 900 bash tools/probes/pmc_sq.sh "$tag" >> "$log" 2>&1
       rc=$?; tail -2 "$log" ;;
     accuracy)
-      env "${libenv[@]}" timeout -k 10 600 python -u tests/debug/accuracy_ab.py "${lib:-head}" > "$log" 2>&1
+      env "${libenv[@]}" timeout -k 10 600 python -u tools/debug/accuracy_ab.py "${lib:-head}" > "$log" 2>&1
       rc=$?; cat "$log" ;;
     probe)
-      timeout -k 10 300 "tests/probes/$arg" > "$log" 2>&1
+      timeout -k 10 300 "tools/probes/$arg" > "$log" 2>&1
       rc=$?; cat "$log" ;;
     *)
       echo "unknown step $step"; exit 2 ;;

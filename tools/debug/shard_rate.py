@@ -6,7 +6,7 @@ per-GPU efficiency those shard times predict for the sharded bench line:
 It measures only the kernels' tail / launch behaviour at 3,062 subgrids per
 GPU (configs[3] at N = 8); RCCL and the host are not in it.
 
-    python tests/debug/shard_rate.py [--steps 10] [--workload default]
+    python tools/debug/shard_rate.py [--steps 10] [--workload default]
 """
 import argparse
 import json

@@ -6,7 +6,7 @@ reference metric, one C = 256 (or argv[1]) -c subgrid.  DESIGN.md §3.1."""
 import sys, numpy as np
 import os
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests", "tests/debug"):
+for _p in ("ska-sdp-idg-bench_amd", "oracle", "tests", "tools/debug"):
     sys.path.insert(0, os.path.join(REPO, _p))
 import idg_amd, oracle as orc
 from phase_reduction_emul import fma32, IH, TAIL, f32

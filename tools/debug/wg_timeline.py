@@ -2,7 +2,7 @@
 (debug build: make BUILD=build_tl LIB=../ab/tl.so EXTRA=-DIDG_WG_TIMELINE=1,
 run with IDG_MI355X_LIB=ab/tl.so IDG_KERNEL_FORM=combined):
 
-    python tests/debug/wg_timeline.py [--counts 3063,24500] [--steps 3]
+    python tools/debug/wg_timeline.py [--counts 3063,24500] [--steps 3]
 
 For the last gridder and degridder launch of `--steps` bench steps over the
 first n subgrids of configs[1] it prints, from the workgroups' own

@@ -5,7 +5,7 @@ least one wait state between an SALU write of M0 and the LDS-DMA that reads
 it as its LDS address (the gfx9 "M0 -> LDS DMA" hazard: hipcc pads it for
 its own code but not inside an asm string), and where the kernels' scratch
 (spill) accesses sit.
-  python tests/probes/dma_drain_check.py LISTING.s"""
+  python tools/probes/dma_drain_check.py LISTING.s"""
 import re
 import sys
 

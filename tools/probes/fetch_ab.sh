@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction)
 # of the MFMA gridder/degridder for library variants:
-#   bash tests/probes/fetch_ab.sh ab/a.so ab/b.so
+#   bash tools/probes/fetch_ab.sh ab/a.so ab/b.so
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 root=$GRAFT_REPO_ROOT/gpurun_out/fetch_ab

@@ -18,7 +18,7 @@ Wait states between producer and consumer: `s_nop N` counts N + 1, every
 other instruction 1.  Paths are followed backwards through labels into every
 branch that targets them.
 
-    python tests/probes/hazard_check.py build/isa/gridder_mi355x.s [...]
+    python tools/probes/hazard_check.py build/isa/gridder_mi355x.s [...]
 """
 import re
 import sys

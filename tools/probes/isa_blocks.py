@@ -1,5 +1,5 @@
 """Per-block instruction counts of one kernel in an ISA listing (debug aid):
-  python tests/probes/isa_blocks.py LISTING.s NAME_PATTERN [FIRST_LINE LAST_LINE]
+  python tools/probes/isa_blocks.py LISTING.s NAME_PATTERN [FIRST_LINE LAST_LINE]
 prints each basic block's label, loop comment, #instructions, #VALU, #s_waitcnt."""
 import re
 import sys

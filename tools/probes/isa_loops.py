@@ -1,6 +1,6 @@
 """Static instruction mix of the MFMA loop bodies of one kernel (ISA listing
 from `make -C ska-sdp-idg-bench_amd isa`).  Usage:
-  python tests/probes/isa_loops.py build/isa/gridder_mi355x.s ILi32ELi4ELi16ELi1E"""
+  python tools/probes/isa_loops.py build/isa/gridder_mi355x.s ILi32ELi4ELi16ELi1E"""
 import re
 import sys
 from collections import Counter

@@ -1,6 +1,6 @@
 """Scratch (spill) instructions inside basic blocks that issue an MFMA, per
 kernel of an ISA listing (the hot loops; make -C ska-sdp-idg-bench_amd isa).
-  python tests/probes/mfma_spills.py LISTING.s"""
+  python tools/probes/mfma_spills.py LISTING.s"""
 import re
 import sys
 

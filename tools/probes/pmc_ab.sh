@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of the gridder for library variants (A/B diagnosis):
-#   bash tests/probes/pmc_ab.sh ab/a.so ab/b.so
+#   bash tools/probes/pmc_ab.sh ab/a.so ab/b.so
 # Output: gpurun_out/pmc_ab/<lib>/p<N>/..., summary printed per library.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,7 +1,7 @@
 """Per-kernel register / scratch / occupancy / LDS summary of a
 -Rpass-analysis=kernel-resource-usage log (make -C ska-sdp-idg-bench_amd isa
 writes build/isa/*.resources.txt).
-  python tests/probes/resources.py ska-sdp-idg-bench_amd/build/isa/*.resources.txt"""
+  python tools/probes/resources.py ska-sdp-idg-bench_amd/build/isa/*.resources.txt"""
 import re
 import sys
 

@@ -1,9 +1,9 @@
-"""Turn the rocprofv3 databases of tests/probes/profile_round.sh and
-tests/probes/pmc_sq.sh (merged back under gpurun_out/) into the committed
+"""Turn the rocprofv3 databases of tools/probes/profile_round.sh and
+tools/probes/pmc_sq.sh (merged back under gpurun_out/) into the committed
 profile summaries and profiles/traffic.json, which bench.py reads for
 `roofline.traffic` and `roofline.issue_bound`.
 
-    python tests/probes/summarize_profiles.py --prof gpurun_out/prof_TAG \
+    python tools/probes/summarize_profiles.py --prof gpurun_out/prof_TAG \
         --pmc gpurun_out/pmc_TAG --out profiles/r01/final [--workload default]
 
 Per kernel (the MFMA gridder/degridder of the workload):
@@ -12,7 +12,7 @@ Per kernel (the MFMA gridder/degridder of the workload):
     correction of MI355X_MICROARCH.md (vector loads tallied at 64 B per
     128-B request), calibrated in profiles/r01/traffic_calibration.md;
   * VALU-issue utilisation: (trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46
-    cycles, tests/probes/instr_rates_probe.hip) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8
+    cycles, tools/probes/instr_rates_probe.hip) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8
     XCDs).
 """
 import argparse
@@ -32,7 +32,7 @@ CYC_TRANS, CYC_MFMA_F16, CYC_VALU = 8.35, 4.7, 4.46
 # Round 4: with the VALU class counters (pmc_sq.sh's optional passes) the
 # "other" VALU is priced per class: v_cvt_pk_f16_f32 (CVT) 4.5, the FMA_F32
 # class 4.58 (v_fma_mix_f32 4.46 and v_pk_fma_f32 4.8 in the loops' 2:1
-# mix, tests/probes/isa_loops.py), everything else at the plain f32 /
+# mix, tools/probes/isa_loops.py), everything else at the plain f32 /
 # integer rate 2.6 (v_fma_f32, v_add_f32, v_mov_b32 2.5-2.7 in
 # instr_rates_probe.hip).
 CYC_CLASS = {"SQ_INSTS_VALU_CVT": 4.5, "SQ_INSTS_VALU_FMA_F32": 4.58}
@@ -228,13 +228,13 @@ def main():
                 other_cyc = (sum(c[k] * v for k, v in CYC_CLASS.items())
                              + plain * CYC_PLAIN)
                 model = ("(trans x 8.35 + f16 MFMA x 4.7 + CVT x 4.5 + FMA_F32 "
-                         "x 4.58 + the rest x 2.6 cycles, tests/probes/"
+                         "x 4.58 + the rest x 2.6 cycles, tools/probes/"
                          "instr_rates_probe.hip) / (GRBM_GUI_ACTIVE / 8 XCDs), "
                          "summed over 1024 SIMDs")
             else:
                 other_cyc = other * CYC_VALU
                 model = ("(trans x 8.35 + f16 MFMA x 4.7 + other VALU x 4.46 "
-                         "cycles, tests/probes/instr_rates_probe.hip) / "
+                         "cycles, tools/probes/instr_rates_probe.hip) / "
                          "(GRBM_GUI_ACTIVE / 8 XCDs), summed over 1024 SIMDs")
             cyc = (c["SQ_INSTS_VALU_TRANS_F32"] * CYC_TRANS
                    + c["SQ_INSTS_VALU_MFMA_F16"] * CYC_MFMA_F16
