@@ -70,17 +70,11 @@ static __constant__ const uint32_t kInvPio4Dev[24] = IDG_INV_PIO4_TABLE;
 #endif
 
 // Entry i of the table.  Every |y| in [120, 2^15) -- all phases the IDG
-// kernels form -- reads i in {0, 1}, 4 + {0, 1} or 8 + {0, 1} (i = bits 26-29
-// of the float), so the device selects those from immediates and reads the
-// constant table only for larger arguments.
+// kernels form -- reads i in {0, 1} (i = bits 26-29 of the float), so the
+// device takes entries i, i + 4, i + 8 for those from immediates (one select
+// each, sincosf_large below) and reads the constant table only otherwise.
 IDG_HD inline uint32_t inv_pio4(uint32_t i) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (i == 0) return 0xa2;
-  if (i == 1) return 0xa2f9;
-  if (i == 4) return 0xf9836e4e;
-  if (i == 5) return 0x836e4e44;
-  if (i == 8) return 0x441529fc;
-  if (i == 9) return 0x1529fc27;
   return kInvPio4Dev[i];
 #else
   static constexpr uint32_t t[24] = IDG_INV_PIO4_TABLE;
@@ -99,24 +93,26 @@ IDG_HD inline uint32_t sincosf_bits(float y) {
 }
 
 // The polynomial pair of s_sincosf.c (sincosf_poly) as the FMA build
-// evaluates it; `neg_cos` selects the second table (quadrants with n & 2),
+// evaluates it, on the reduced argument r (x2 = r * r).  glibc multiplies r by
+// sign[n & 3] before the sine polynomial and takes the second table (c0..c4
+// negated, s1..s3 the same) for quadrants with n & 2; every step of either
+// polynomial is sign-symmetric (round to nearest even), so that is exactly
+// the negation of the float result: `neg_sin` / `neg_cos` apply it there, and
 // `swap` exchanges sin and cos (odd n).
-IDG_HD inline void sincosf_poly(double x, double x2, bool neg_cos, bool swap,
-                                float *sinp, float *cosp) {
-  const double c0 = neg_cos ? -kSincosfC0 : kSincosfC0;
-  const double c1 = neg_cos ? -kSincosfC1 : kSincosfC1;
-  const double c2 = neg_cos ? -kSincosfC2 : kSincosfC2;
-  const double c3 = neg_cos ? -kSincosfC3 : kSincosfC3;
-  const double c4 = neg_cos ? -kSincosfC4 : kSincosfC4;
-  const double x3 = x2 * x, x4 = x2 * x2;
+IDG_HD inline void sincosf_poly(double r, double x2, bool neg_sin,
+                                bool neg_cos, bool swap, float *sinp,
+                                float *cosp) {
+  const double x3 = x2 * r, x4 = x2 * x2;
   const double s1p = sincosf_fma(x2, kSincosfS3, kSincosfS2);
-  const double c2p = sincosf_fma(x2, c4, c3);
-  const double c1p = sincosf_fma(x2, c1, c0);
+  const double c2p = sincosf_fma(x2, kSincosfC4, kSincosfC3);
+  const double c1p = sincosf_fma(x2, kSincosfC1, kSincosfC0);
   const double x5 = x2 * x3, x6 = x2 * x4;
-  const double s = sincosf_fma(x3, kSincosfS1, x);
-  const double c = sincosf_fma(x4, c2, c1p);
-  const float so = static_cast<float>(sincosf_fma(x5, s1p, s));
-  const float co = static_cast<float>(sincosf_fma(x6, c2p, c));
+  const double s = sincosf_fma(x3, kSincosfS1, r);
+  const double c = sincosf_fma(x4, kSincosfC2, c1p);
+  float so = static_cast<float>(sincosf_fma(x5, s1p, s));
+  float co = static_cast<float>(sincosf_fma(x6, c2p, c));
+  so = neg_sin ? -so : so;
+  co = neg_cos ? -co : co;
   *sinp = swap ? co : so;
   *cosp = swap ? so : co;
 }
@@ -132,38 +128,32 @@ IDG_HD inline double sincosf_i64_to_double(int64_t res) {
 #endif
 }
 
-// glibc 2.35 sincosf(y, sinp, cosp) for finite y.
-IDG_HD inline void sincosf_glibc(float y, float *sinp, float *cosp) {
-  const uint32_t bits = sincosf_bits(y);
-  const uint32_t top = (bits >> 20) & 0x7ff;
-  const double x = static_cast<double>(y);
-  if (top <= 0x397) {  // |y| < 2^-12
-    *sinp = y;
-    *cosp = 1.0f;
-    return;
-  }
-  if (top <= 0x3f3) {  // |y| < pi/4
-    sincosf_poly(x, x * x, false, false, sinp, cosp);
-    return;
-  }
-  if (top <= 0x42e) {  // |y| < 120
-    const int n =
-        (static_cast<int32_t>(x * kSincosfHpiInv) + 0x800000) >> 24;
-    const double r = sincosf_fma(-static_cast<double>(n), kSincosfHpi, x);
-    const double s = ((n + 1) & 2) ? -1.0 : 1.0;  // sign[n & 3]: 1,-1,-1,1
-    sincosf_poly(r * s, r * r, (n & 2) != 0, (n & 1) != 0, sinp, cosp);
-    return;
-  }
-  if (top >= 0x7f8) {  // inf / nan: nan, as glibc's y - y
-    *sinp = *cosp = y - y;
-    return;
-  }
+// The large-argument class (120 <= |y| < inf): glibc's reduce_large, then
+// the polynomials.  For |y| < 2^15 (i <= 1) the three table entries are
+// selected from immediates.
+IDG_HD inline void sincosf_large(uint32_t bits, float *sinp, float *cosp) {
   const uint32_t sign = bits >> 31;
   const uint32_t i = (bits >> 26) & 15;
   const uint32_t xi = ((bits & 0x7fffff) | 0x800000) << ((bits >> 23) & 7);
-  const uint64_t res0w = static_cast<uint32_t>(xi * inv_pio4(i));
-  const uint64_t res1 = static_cast<uint64_t>(xi) * inv_pio4(i + 4);
-  const uint64_t res2 = static_cast<uint64_t>(xi) * inv_pio4(i + 8);
+  uint32_t a0, a4, a8;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (i <= 1) {
+    a0 = i ? 0xa2f9u : 0xa2u;
+    a4 = i ? 0x836e4e44u : 0xf9836e4eu;
+    a8 = i ? 0x1529fc27u : 0x441529fcu;
+  } else {
+    a0 = inv_pio4(i);
+    a4 = inv_pio4(i + 4);
+    a8 = inv_pio4(i + 8);
+  }
+#else
+  a0 = inv_pio4(i);
+  a4 = inv_pio4(i + 4);
+  a8 = inv_pio4(i + 8);
+#endif
+  const uint64_t res0w = static_cast<uint32_t>(xi * a0);
+  const uint64_t res1 = static_cast<uint64_t>(xi) * a4;
+  const uint64_t res2 = static_cast<uint64_t>(xi) * a8;
   uint64_t res0 = (res2 >> 32) | (res0w << 32);
   res0 += res1;
   const uint64_t n = (res0 + (1ULL << 61)) >> 62;
@@ -171,8 +161,34 @@ IDG_HD inline void sincosf_glibc(float y, float *sinp, float *cosp) {
   const double r =
       sincosf_i64_to_double(static_cast<int64_t>(res0)) * kSincosfPi63;
   const uint32_t q = static_cast<uint32_t>(n) + sign;
-  const double s = ((q + 1) & 2) ? -1.0 : 1.0;
-  sincosf_poly(r * s, r * r, (q & 2) != 0, (n & 1) != 0, sinp, cosp);
+  // sign[q & 3] = 1, -1, -1, 1; the second table for q & 2; swap for odd n
+  sincosf_poly(r, r * r, ((q + 1) & 2) != 0, (q & 2) != 0, (n & 1) != 0,
+               sinp, cosp);
+}
+
+// glibc 2.35 sincosf(y, sinp, cosp).
+IDG_HD inline void sincosf_glibc(float y, float *sinp, float *cosp) {
+  const uint32_t bits = sincosf_bits(y);
+  const uint32_t top = (bits >> 20) & 0x7ff;
+  if (top > 0x42e && top < 0x7f8) {  // 120 <= |y| < inf: the common case
+    sincosf_large(bits, sinp, cosp);
+    return;
+  }
+  const double x = static_cast<double>(y);
+  if (top <= 0x397) {  // |y| < 2^-12
+    *sinp = y;
+    *cosp = 1.0f;
+  } else if (top <= 0x3f3) {  // |y| < pi/4
+    sincosf_poly(x, x * x, false, false, false, sinp, cosp);
+  } else if (top <= 0x42e) {  // |y| < 120
+    const int n =
+        (static_cast<int32_t>(x * kSincosfHpiInv) + 0x800000) >> 24;
+    const double r = sincosf_fma(-static_cast<double>(n), kSincosfHpi, x);
+    sincosf_poly(r, r * r, ((n + 1) & 2) != 0, (n & 2) != 0, (n & 1) != 0,
+                 sinp, cosp);
+  } else {  // inf / nan: nan, as glibc's y - y
+    *sinp = *cosp = y - y;
+  }
 }
 
 }  // namespace idg

@@ -77,6 +77,26 @@ __device__ __forceinline__ void mac_ref(float (&a)[8], const float4 &va,
   }
 }
 
+// The same for a base pixel (phasor (c, s)) and its mirror (phasor (c, -s),
+// exactly: the mirror phase is the negated base phase and sincosf is odd /
+// even), sharing the products: vi * (-s) = -(vi * s) exactly, so the
+// mirror's fma(vr, c, -(vi * (-s))) is fma(vr, c, vi * s).
+__device__ __forceinline__ void mac_ref_pair(float (&a)[8], float (&b)[8],
+                                             const float4 &va,
+                                             const float4 &vb, float cs,
+                                             float sn) {
+  const float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float vr = v[2 * q], vi = v[2 * q + 1];
+    const float t1 = vi * sn, t2 = vr * sn;
+    a[2 * q] = a[2 * q] + fma_(vr, cs, -t1);
+    a[2 * q + 1] = a[2 * q + 1] + fma_(vi, cs, t2);
+    b[2 * q] = b[2 * q] + fma_(vr, cs, t1);
+    b[2 * q + 1] = b[2 * q + 1] + fma_(vi, cs, -t2);
+  }
+}
+
 // Output pixel p: sph * (A1^H P A2) with the reference's forms (common/
 // math.hpp apply_aterm_gridder), correlation-planar store.
 __device__ __forceinline__ void seq_store_pixel(
@@ -151,13 +171,22 @@ __device__ __forceinline__ void seq_grid_pixels(
         const float ph = fma_(-pidx[i], k, po[i]);
         float sn, cs;
         idg::sincosf_glibc(ph, &sn, &cs);
-        mac_ref(acc[i], va, vb, cs, sn);
         if constexpr (MIRROR) {
+          // the mirror's own phase, formed as the reference forms it; where
+          // it is the exact negation (every lane of every wave on the
+          // benchmark data) one sincosf and one set of products serve both
           const float phm = fma_(-pidx[NP + i], k, po[NP + i]);
-          float snm = -sn, csm = cs;
-          if (fbits(phm) != (fbits(ph) ^ 0x80000000u))
-            idg::sincosf_glibc(phm, &snm, &csm);
-          mac_ref(acc[NP + i], va, vb, csm, snm);
+          const bool neg = fbits(phm) == (fbits(ph) ^ 0x80000000u);
+          if (__all(neg)) {
+            mac_ref_pair(acc[i], acc[NP + i], va, vb, cs, sn);
+          } else {
+            float snm = -sn, csm = cs;
+            if (!neg) idg::sincosf_glibc(phm, &snm, &csm);
+            mac_ref(acc[i], va, vb, cs, sn);
+            mac_ref(acc[NP + i], va, vb, csm, snm);
+          }
+        } else {
+          mac_ref(acc[i], va, vb, cs, sn);
         }
       }
     }
