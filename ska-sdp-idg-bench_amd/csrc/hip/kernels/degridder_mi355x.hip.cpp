@@ -689,6 +689,13 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
 // K-block of the 512), so an S = 32 subgrid is one chunk and its
 // visibilities are written once (the combined kernel's 512-pixel chunks
 // read them back and wrote them again).
+// IDG_DEGRID_KP64=512: the S = 64 8-wave mirror kernel keeps 512-pair
+// chunks (A/B); the two-kernel form takes the 8-wave one at S = 64
+#ifndef IDG_DEGRID_KP64
+#define IDG_DEGRID_KP64 1024
+#endif
+constexpr int mirror_kp64() { return IDG_DEGRID_KP64; }
+
 template <int S_CT, int CT, int NW, bool TAIL = true>
 __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
     kernel_degridder_mirror_mi355x(
@@ -701,7 +708,12 @@ __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
         const float2 *__restrict__ aterms,
         const idg::Metadata *__restrict__ metadata,
         const float2 *__restrict__ subgrids, int *__restrict__ queue) {
-  constexpr int KP = 512;
+  // S = 64 on 8 waves: 1,024-pair chunks (80 KB of LDS, two workgroups per
+  // CU: the occupancy of four 4-wave ones), so a subgrid is two chunks, not
+  // four, and its visibilities are written, read back and written again
+  // once instead of three times (profiles/r04/kernels_s64: 18.7 GB per
+  // launch against 4.85 GB algorithmic)
+  constexpr int KP = (S_CT == 64 && NW == 8) ? mirror_kp64() : 512;
   __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
@@ -891,7 +903,10 @@ KernelChoice select_degridder(const Problem &p) {
     if (IDG_DEGRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
       // mirror-eligible subgrids (even S only), then the others on 8-wave
       // workgroups with 1,024-pixel chunks
-      if (p.subgrid_size % 2 == 0)
+      if (s64 && mirror_kp64() > 512)  // 8 waves, 1,024-pair chunks
+        k.parts[0] = {degridder_set_for<64>(true, tail).mirror, 512,
+                      KernelChoice::kMirror};
+      else if (p.subgrid_size % 2 == 0)
         k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror};
       k.parts[1] = {set.general, 512, KernelChoice::kGeneral};
       k.all_general = {set.general_direct, 512, KernelChoice::kPlain};

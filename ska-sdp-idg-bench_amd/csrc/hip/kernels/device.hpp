@@ -176,9 +176,12 @@ __host__ __device__ inline size_t queue_ints(int ns) {
   return kQueueHead + static_cast<size_t>(kQueueShards) * queue_cap(ns);
 }
 
-// One thread of the pushing workgroup.
-__device__ __forceinline__ void queue_push(int *queue, int ns, int s) {
-  const int x = blockIdx.x % kQueueShards;
+// One thread of the pushing workgroup; shard x (default: the workgroup's
+// XCD, blockIdx % 8).  A shard takes at most queue_cap(ns) entries: a
+// launch with several workgroups per subgrid pushes into shard s % 8.
+__device__ __forceinline__ void queue_push(int *queue, int ns, int s,
+                                           int shard = -1) {
+  const int x = shard >= 0 ? shard : static_cast<int>(blockIdx.x) % kQueueShards;
   queue[kQueueHead + x * queue_cap(ns) + atomicAdd(queue + 32 * x, 1)] = s;
 }
 

@@ -63,6 +63,10 @@
 #ifndef IDG_GRID_BSCALE
 #define IDG_GRID_BSCALE 12
 #endif
+// non-temporal B-fill loads (A/B; see the fill loop)
+#ifndef IDG_GRID_NT_FILL
+#define IDG_GRID_NT_FILL 0
+#endif
 // waves per workgroup of the MFMA kernel (the VALU kernel uses kBlock)
 #ifndef IDG_GRID_NW
 #define IDG_GRID_NW 8
@@ -319,7 +323,8 @@ __device__ __forceinline__ void grid_mfma(
     const float *__restrict__ wavenumbers,
     const float2 *__restrict__ visibilities,
     const float *__restrict__ spheroidal, const float2 *__restrict__ aterms,
-    float2 *__restrict__ out, unsigned *lds, float vmax_pre = 0.0f) {
+    float2 *__restrict__ out, unsigned *lds, float vmax_pre = 0.0f,
+    int pass_lo = 0, int pass_hi = 1 << 30) {
   static_assert(CB % 4 == 0, "anchor blocks hold whole channel quads");
   // General path: an opaque copy of the thread index, so values derived
   // from it are formed per call, not hoisted out of the general kernel's
@@ -404,7 +409,10 @@ __device__ __forceinline__ void grid_mfma(
   float4 *tuvw = reinterpret_cast<float4 *>(lds + Lds::kUvwOff);
 
   constexpr int kPass = NW * 16 * PT;  // base pixels per pass
-  for (int gbase = 0; gbase < half; gbase += kPass) {
+  // [pass_lo, pass_hi): the base pixels this workgroup takes (a multiple of
+  // kPass; all of them unless the subgrid's passes are split over
+  // workgroups, kernel_gridder_mirror_mi355x SPLIT)
+  for (int gbase = pass_lo; gbase < min(half, pass_hi); gbase += kPass) {
     // Pixel terms of tile pairs (2h, 2h+1), packed: every phase operation
     // below is one v_pk_* over the pair with the channel's wavenumber
     // broadcast from an SGPR, so no operand has to be duplicated.
@@ -524,10 +532,26 @@ __device__ __forceinline__ void grid_mfma(
                   vsubf + ((q0 + qq) * 4 * C + c0) * 8);
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
+#if IDG_GRID_NT_FILL
+                // the fill is the rows' last use: non-temporal (a raw buffer
+                // load keeps the SGPR-base + VGPR-offset form), so L2 keeps
+                // the blocked-summation masters rather than spent rows
+                const __amdgpu_buffer_rsrc_t rsrc =
+                    __builtin_amdgcn_make_buffer_rsrc(
+                        const_cast<char *>(blk), static_cast<short>(0),
+                        0x7ffffff0, 0x00020000);
+                const float rc = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(
+                               rsrc, static_cast<int>(off_c), 32 * u, 2));
+                const float rs = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(
+                               rsrc, static_cast<int>(off_s), 32 * u, 2));
+#else
                 const float rc =
                     *reinterpret_cast<const float *>(blk + off_c + 32 * u);
                 const float rs =
                     *reinterpret_cast<const float *>(blk + off_s + 32 * u);
+#endif
                 lmax = fmaxf(lmax, fmaxf(fabsf(rc), fabsf(rs)));
                 bc[u] = rc * scale;
                 bs[u] = rs * sc_s;
@@ -1113,7 +1137,16 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 //   workgroup returns at once.
 // queue: device.hpp queue_ints(nr_subgrids) ints of stream-ordered
 // workspace, its counters zeroed before the launches.
-template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
+// SPLIT > 1 (S = 64: four passes of 512 base pixels): grid = SPLIT x
+// nr_subgrids, workgroup (s, q) takes pass q of subgrid s.  The SPLIT
+// workgroups of a subgrid are consecutive in the XCD-contiguous order, so
+// they run side by side on one XCD and all but the first read the subgrid's
+// visibilities from its L2 -- one pass after another in one workgroup
+// re-streamed them from memory each pass (2.0x the algorithmic bytes,
+// profiles/r04/kernels_s64).  Each workgroup forms the same scale from the
+// same first fill, so the output is the one-workgroup kernel's.
+template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail,
+          int SPLIT = 1>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     kernel_gridder_mirror_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -1129,7 +1162,9 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
   __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
-  const int s = xcd_subgrid(blockIdx.x, gridDim.x);
+  const int wg = xcd_subgrid(blockIdx.x, gridDim.x);
+  const int s = SPLIT > 1 ? wg / SPLIT : wg;
+  const int q = SPLIT > 1 ? wg % SPLIT : 0;
   const int tid = threadIdx.x;
   const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S, image_size,
                                        w_step_in_lambda);
@@ -1139,14 +1174,21 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
                                          red)) == 0 &&
       S % 2 == 0 && g.w_offset == 0.0f;
   if (!mirror) {
-    if (tid == 0) queue_push(queue, gridDim.x, s);
+    if constexpr (SPLIT > 1) {
+      if (tid == 0 && q == 0)
+        queue_push(queue, gridDim.x / SPLIT, s, s % kQueueShards);
+    } else {
+      if (tid == 0) queue_push(queue, gridDim.x, s);
+    }
     return;
   }
+  constexpr int kPass = NW * 16 * PT;
   grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds,
-      prologue_max<NW>(red));
+      prologue_max<NW>(red), SPLIT > 1 ? q * kPass : 0,
+      SPLIT > 1 ? (q + 1) * kPass : 1 << 30);
 }
 
 template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
@@ -1206,12 +1248,21 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
 struct GridderSet {
   const void *combined, *mirror, *general;
 };
+// The mirror kernel's workgroups per subgrid: the four S = 64 passes on
+// four workgroups (IDG_GRID_SPLIT64=0: one, the A/B).
+#ifndef IDG_GRID_SPLIT64
+#define IDG_GRID_SPLIT64 1
+#endif
+constexpr int mirror_split(int S) {
+  return S == 64 && IDG_GRID_SPLIT64 ? 4 : 1;
+}
 template <int S_, int PPT_, bool FFT_, int PREC_>
 GridderSet gridder_set() {
   return {reinterpret_cast<const void *>(
               &kernel_gridder_mi355x<S_, PPT_, 16, 1, IDG_GRID_PT, FFT_, PREC_>),
           reinterpret_cast<const void *>(
-              &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_>),
+              &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_,
+                                            mirror_split(S_)>),
           reinterpret_cast<const void *>(
               &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_>)};
 }
@@ -1309,7 +1360,9 @@ KernelChoice select_gridder(const Problem &p) {
   }
   k.func = set.combined;
   if (mfma && IDG_GRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
-    if (set.mirror) k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror};
+    if (set.mirror)
+      k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror,
+                    p.subgrid_size == 64 ? mirror_split(64) : 1};
     k.parts[1] = {set.general, k.block, KernelChoice::kGeneral};
     // no subgrid mirror-eligible: the combined kernel, one workgroup per
     // subgrid (2.7 % faster on a w-term batch than the queue-fed kernel)

@@ -462,8 +462,9 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
   for (int i = 0; i < 13; ++i) args[i] = args13[i];
   args[13] = &queue;
   if (err == hipSuccess && run_mirror)
-    err = hipLaunchKernel(mirror.func, dim3(nr_subgrids), dim3(mirror.block),
-                          args, 0, stream);
+    err = hipLaunchKernel(mirror.func,
+                          dim3(nr_subgrids * std::max(1, mirror.per_subgrid)),
+                          dim3(mirror.block), args, 0, stream);
   args[14] = &ns;
   args[15] = &all;
   if (err == hipSuccess)

@@ -137,6 +137,7 @@ struct KernelChoice {
     const void *func = nullptr;
     int block = 0;
     int kind = kPlain;
+    int per_subgrid = 1;  // workgroups per subgrid (mirror part: grid x)
   } parts[2], all_general;
 };
 

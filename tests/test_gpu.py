@@ -923,6 +923,43 @@ def test_queue_workspace_reused_across_launches(idg, full_mixed, op,
         assert torch.equal(out, first)
 
 
+@pytest.mark.parametrize("wmix", [False, True])
+def test_s64_mirror_passes_on_four_workgroups_bitwise(idg, wmix,
+                                                      monkeypatch):
+    """S = 64: the two-kernel form's mirror kernel runs each subgrid's four
+    512-pixel passes on four workgroups side by side (kernel_gridder_mirror_
+    mi355x SPLIT = 4; they share the visibilities through L2); its output is
+    the combined kernel's, one workgroup per subgrid, bit for bit -- with
+    every third subgrid w != 0 too (queued from pass 0's workgroup only)."""
+    import torch
+    st, ts, T, C, G, S = 50, 8, 32, 16, 1024, 64
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    if wmix:
+        a["uvw"][1::3, :, 2] = 41.0
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    assert p["nr_subgrids"] >= 8192  # the two-kernel form
+    dev = _to_device(a)
+    outs = {}
+    for form in ("split", "combined"):
+        monkeypatch.setenv("IDG_KERNEL_FORM", form)
+        outs[form] = _dgrid(idg, p, dev, dev["visibilities"])
+    torch.cuda.synchronize()
+    assert torch.equal(outs["split"], outs["combined"])
+    s = p["nr_subgrids"] - 1
+    go = np.zeros((1, 4, S, S, 2), np.float32)
+    md0 = a["metadata"][s:s + 1].copy()
+    md0["time_offset"] = 0
+    import oracle as orc
+    orc.Oracle().gridder(*_params(dict(p, nr_subgrids=1)),
+                         np.ascontiguousarray(a["uvw"][s]), a["wavenumbers"],
+                         np.ascontiguousarray(a["visibilities"][s]),
+                         a["spheroidal"], a["aterms"], md0, go)
+    g = outs["split"][s:s + 1].cpu().numpy()
+    assert orc.Oracle().check_error(g, go)[0] <= TOLERANCE
+
+
 def test_workspaces_released_with_their_stream(idg, full_mixed,
                                                monkeypatch):
     """idg_release_workspaces: the split-form launches on a private stream

@@ -196,3 +196,47 @@ def test_restated_harness_sequential_c256(exe):
         capture_output=True, text=True, timeout=300)
     assert ">>> Result PASSED" in r.stdout, r.stdout[-2000:] + r.stderr
     assert r.returncode == 0
+
+
+@pytest.mark.timeout(600)
+def test_sequential_full_configs4_batch_samples_bit_exact(idg, oracle_lib,
+                                                          sequential):
+    """BASELINE configs[4] at full size (S = 64, 24,500 subgrids) on the
+    sequential kernels through the device entries: sampled subgrids and
+    their visibility rows bit-exact to the oracle (itself bit-exact to
+    app/CPU)."""
+    import torch
+    st, ts, T, C, G, S = 50, 20, 128, 16, 1024, 64
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    ns = idg.nr_subgrids_for(st, ts)
+    p = dict(nr_subgrids=ns, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    dev = {k: torch.from_numpy(v).cuda() for k, v in a.items()
+           if k not in ("metadata", "frequencies")}
+    dev["metadata"] = torch.from_numpy(
+        a["metadata"].view(np.int32).reshape(-1, 9).copy()).cuda()
+    g_dev = torch.empty_like(dev["subgrids"])
+    idg.gridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"],
+                       dev["visibilities"], dev["spheroidal"], dev["aterms"],
+                       dev["metadata"], g_dev)
+    d_dev = torch.empty_like(dev["visibilities"])
+    idg.degridder_launch(*_params(p), dev["uvw"], dev["wavenumbers"], d_dev,
+                         dev["spheroidal"], dev["aterms"], dev["metadata"],
+                         dev["subgrids"])
+    torch.cuda.synchronize()
+    q = dict(p, nr_subgrids=1)
+    for s in (0, ns // 2 + 3, ns - 1):
+        md0 = a["metadata"][s:s + 1].copy()
+        md0["time_offset"] = 0
+        uvw = np.ascontiguousarray(a["uvw"][s])
+        go = np.zeros((1, 4, S, S, 2), np.float32)
+        oracle_lib.gridder(*_params(q), uvw, a["wavenumbers"],
+                           np.ascontiguousarray(a["visibilities"][s]),
+                           a["spheroidal"], a["aterms"], md0, go)
+        do = np.zeros((1, T, C, 4, 2), np.float32)
+        oracle_lib.degridder(*_params(q), uvw, a["wavenumbers"], do,
+                             a["spheroidal"], a["aterms"], md0,
+                             np.ascontiguousarray(a["subgrids"][s:s + 1]))
+        assert _mismatch(g_dev[s:s + 1].cpu().numpy(), go) == 0, s
+        assert _mismatch(d_dev[s:s + 1].cpu().numpy(), do) == 0, s
