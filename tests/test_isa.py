@@ -126,9 +126,12 @@ def test_l2_prefetch_is_not_drained_before_the_mfma_loop(listings):
         checked.append(k)
         assert total > 0 and drained == 0, (k, total, drained)
     # every precision variant (the last template argument, device.hpp kPrec*)
-    for form in ("gridder_mirror<32,16,4,", "gridder_general<32,16,4,"):
-        for prec in ("0>", "1>", "3>"):
-            assert form + prec in checked, checked
+    # (the mirror kernel's last argument is SPLIT, its workgroups per
+    # subgrid: 1 at S = 32)
+    for form, tail in (("gridder_mirror<32,16,4,", ",1>"),
+                       ("gridder_general<32,16,4,", ">")):
+        for prec in ("0", "1", "3"):
+            assert form + prec + tail in checked, checked
 
 
 def test_lds_dma_m0_wait_state_checker():
