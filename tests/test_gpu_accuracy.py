@@ -220,3 +220,55 @@ def test_c_defaults_closer_to_exact_than_the_reference(idg, oracle_lib,
         # the lo parts of small pixels in f16 subnormals): held to 1.25x
         assert split["ours_vs_exact"] <= 1.25 * split["ref_vs_exact"], \
             fmt(split)
+
+
+@pytest.mark.parametrize("C", [16, 64])
+def test_tail_patterns_on_channel_incoherent_visibilities(idg, oracle_lib,
+                                                          C, monkeypatch):
+    """The default gridder tail (kPrecTailAlt: 4x the reduction tail on one
+    channel per quad) cancels to first order where a quad's four terms are
+    coherent, as on the reference's synthetic data.  Here every channel of
+    every timestep gets an independent random phase (a worst case for that
+    cancellation).  Measured (profiles/r05/accuracy/): the
+    alternating tail is then the worst of the three -- 1.31e-6 / 2.43e-6 at
+    C = 16 / 64 against 1.02e-6 / 1.95e-6 with none and 0.43e-6 / 1.33e-6
+    with the tail on every phasor (kPrecTail), the reference's own f32 sum
+    0.79e-6 / 2.21e-6 -- but every pattern stays within half the bar
+    against exact accumulation.  The default keeps the alternating tail for
+    its 5 %; IDG_PREC=1 selects the every-phasor one."""
+    import torch
+    st, ts, T, G, S = 2, 2, 128, 1024, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    rng = np.random.default_rng(23)
+    ph = rng.uniform(0.0, 2 * np.pi, a["visibilities"].shape[:3])
+    rot = np.stack([np.cos(ph), np.sin(ph)], -1).astype(np.float32)
+    v = a["visibilities"]  # [..., C, 4, 2]: rotate every (t, c) by its phase
+    vr, vi = v[..., 0].copy(), v[..., 1].copy()
+    c_, s_ = rot[..., None, 0], rot[..., None, 1]
+    v[..., 0] = vr * c_ - vi * s_
+    v[..., 1] = vr * s_ + vi * c_
+    ns = a["metadata"].size
+    p = (ns, G, S, idg.IMAGE_SIZE, 0.0, C, st)
+    exact = np.zeros((ns, 4, S, S, 2), np.float64)
+    oracle_lib.gridder_exact(*p, a["uvw"], a["wavenumbers"], v,
+                             a["spheroidal"], a["aterms"], a["metadata"],
+                             exact, nthreads=8)
+    ex32 = exact.astype(np.float32)
+    errs = {}
+    for name, bits in (("tail_alt", "4"), ("tail_every", "1"), ("none", "0")):
+        monkeypatch.setenv("IDG_PREC", bits)
+        out = np.zeros((ns, 4, S, S, 2), np.float32)
+        idg.c_run_gridder(*p, a["uvw"], a["wavenumbers"], v, a["spheroidal"],
+                          a["aterms"], a["metadata"], out)
+        errs[name] = oracle_lib.check_error(out, ex32)[0]
+    ref = np.zeros((ns, 4, S, S, 2), np.float32)
+    oracle_lib.gridder(*p, a["uvw"], a["wavenumbers"], v, a["spheroidal"],
+                       a["aterms"], a["metadata"], ref)
+    errs["reference_order_f32"] = oracle_lib.check_error(ref, ex32)[0]
+    print(f"C={C} channel-incoherent visibilities, vs exact:",
+          {k: f"{e:.3e}" for k, e in errs.items()})
+    _record(f"tail_patterns_incoherent_c{C}", errs)
+    for k in ("tail_alt", "tail_every", "none"):
+        assert errs[k] <= 0.5 * TOLERANCE, errs
+    # the every-phasor tail removes the systematic part on any data
+    assert errs["tail_every"] <= errs["none"], errs
