@@ -133,6 +133,55 @@ def test_geometry_sweep_vs_oracle(idg, oracle_lib, geom):
     assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
 
 
+@pytest.mark.parametrize("image_size", [0.002, 0.03, 0.08])
+@pytest.mark.parametrize("S", [32, 64])
+def test_image_size_vs_oracle(idg, oracle_lib, image_size, S):
+    # the field of view scales the phase index (|phase| ~ 8x the default at
+    # 0.08): the kernels' phase reduction and the two-term split stay within
+    # the reference metric of the oracle on the same inputs
+    st, ts, T, C, G = 3, 2, 16, 8, 512
+    a = idg.generate(st, ts, T, C, G, S)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=image_size, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    g = _grid(idg, p, a)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"],
+                       a["metadata"], go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], a["metadata"],
+                         a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+@pytest.mark.parametrize("G", [2048, 8192])
+def test_large_grid_vs_oracle(idg, oracle_lib, G):
+    # larger grids: subgrid corners far from the centre (phase offsets up to
+    # ~1e4 rad) and the generator's uvw radii in [G/2, G) (phase indices ~8x
+    # the default at G = 8192)
+    st, ts, T, C, S = 3, 2, 16, 8, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    g = _grid(idg, p, a)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"],
+                       a["metadata"], go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], a["metadata"],
+                         a["subgrids"])
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
 W_SWEEP = [
     (3, 2, 16, 8, 512, 32),
     (2, 1, 9, 7, 256, 24),
@@ -239,8 +288,8 @@ def test_mixed_mirror_and_general_subgrids_in_one_launch(idg, oracle_lib,
 
 
 def test_empty_and_ragged_subgrids(idg, oracle_lib):
-    # nr_timesteps = 0 subgrids, ragged timestep counts, non-zero
-    # baseline offsets and A-term slots
+    # nr_timesteps = 0 subgrids, ragged timestep counts and A-term slots
+    # (non-zero baseline offsets: test_baseline_offsets_vs_oracle)
     st, ts, T, C, G, S = 3, 2, 10, 4, 256, 16
     a = idg.generate(st, ts, T, C, G, S)
     md = a["metadata"].copy()
@@ -264,6 +313,51 @@ def test_empty_and_ragged_subgrids(idg, oracle_lib):
                          a["spheroidal"], a["aterms"], md, a["subgrids"])
     # rows not referenced stay untouched, referenced rows match
     assert np.array_equal(d == sentinel, do == sentinel)
+    assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
+
+
+def _rebase(md, first=1000):
+    """Baseline offsets that are not zero, metadata[0]'s included, with the
+    time offsets moved so that every subgrid keeps its rows: the reference's
+    time index is (baseline_offset - metadata[0].baseline_offset) +
+    time_offset (gridder_reference.cpp:16-25)."""
+    md = md.copy()
+    s = np.arange(md.size)
+    # steps larger than a subgrid's rows, so some time offsets go negative
+    bo = first + s * (3 * int(md["nr_timesteps"].max()) + 7)
+    rows = md["time_offset"].astype(np.int64) + md["baseline_offset"] - \
+        md["baseline_offset"][0]
+    md["baseline_offset"] = bo
+    md["time_offset"] = rows - (bo - bo[0])
+    return md
+
+
+@pytest.mark.parametrize("geom", [(3, 2, 16, 8, 512, 32), (2, 2, 9, 5, 256, 64),
+                                  (3, 1, 7, 3, 256, 33)])
+def test_baseline_offsets_vs_oracle(idg, oracle_lib, geom):
+    # metadata[0].baseline_offset != 0 and offsets that vary by subgrid: the
+    # kernels rebase the time index exactly as the reference does, so the
+    # outputs are those of the same batch with zero offsets, and match the
+    # oracle on the rebased metadata
+    st, ts, T, C, G, S = geom
+    a = idg.generate(st, ts, T, C, G, S)
+    md = _rebase(a["metadata"])
+    assert md["baseline_offset"][0] != 0
+    assert md.size == 1 or (md["time_offset"] < 0).any()
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    g = _grid(idg, p, a, md=md)
+    assert np.array_equal(g, _grid(idg, p, a))
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"],
+                       a["visibilities"], a["spheroidal"], a["aterms"], md, go)
+    assert oracle_lib.check_error(g, go)[0] <= TOLERANCE
+    d = _degrid(idg, p, a, md=md)
+    assert np.array_equal(d, _degrid(idg, p, a))
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], md, a["subgrids"])
     assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
 
 

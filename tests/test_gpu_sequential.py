@@ -123,6 +123,35 @@ def test_sequential_bit_exact_with_w_terms(idg, oracle_lib, sequential, geom):
     assert _mismatch(_degrid(idg, p, a, md), do) == 0
 
 
+def test_sequential_bit_exact_with_baseline_offsets(idg, oracle_lib,
+                                                    sequential):
+    # metadata[0].baseline_offset != 0, offsets varying by subgrid, negative
+    # time offsets: the reference's time index, bit for bit
+    from test_gpu import _rebase
+    st, ts, T, C, G, S = 3, 2, 16, 8, 512, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    md = _rebase(a["metadata"])
+    p = dict(nr_subgrids=md.size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    go, do = _oracle(oracle_lib, p, a, md)
+    assert _mismatch(_grid(idg, p, a, md), go) == 0
+    assert _mismatch(_degrid(idg, p, a, md), do) == 0
+
+
+@pytest.mark.parametrize("image_size", [0.002, 0.08])
+def test_sequential_bit_exact_at_other_image_sizes(idg, oracle_lib,
+                                                   sequential, image_size):
+    st, ts, T, C, G, S = 3, 2, 16, 8, 512, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=image_size, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    go, do = _oracle(oracle_lib, p, a)
+    assert _mismatch(_grid(idg, p, a), go) == 0
+    assert _mismatch(_degrid(idg, p, a), do) == 0
+
+
 def test_sequential_mirror_fallback_on_mixed_w(idg, oracle_lib, sequential):
     # w != 0 on some subgrids only: mirror and single-pixel subgrids in one
     # launch; plus empty and ragged subgrids
