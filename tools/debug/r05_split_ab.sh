@@ -4,6 +4,8 @@
 # (IDG_SPLIT_FFT=rows): the bit-equality tests, then the bench's pipeline
 # timings at configs[1] and configs[4], interleaved, two reps each, then a
 # kernel trace of both.
+# (The lanes kernel was removed after this A/B: profiles/r05/rejected/.  On
+# today's tree IDG_SPLIT_FFT=1 and =rows both run the four-plane kernel.)
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r05_split; mkdir -p $out
