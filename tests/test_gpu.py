@@ -182,6 +182,41 @@ def test_large_grid_vs_oracle(idg, oracle_lib, G):
     assert oracle_lib.check_error(d, do)[0] <= TOLERANCE
 
 
+@pytest.mark.parametrize("bad", [np.nan, np.inf])
+@pytest.mark.parametrize("impl", ["", "sequential"])
+def test_non_finite_inputs_propagate_as_the_oracle(idg, oracle_lib, bad, impl,
+                                                   monkeypatch):
+    # one NaN / Inf visibility component (gridder) or subgrid pixel
+    # (degridder): the reference's sums carry it into every pixel /
+    # visibility of that subgrid, as NaN (Inf meets -Inf in the 2x2 products
+    # and the phasor sums); the kernels' non-finite values sit exactly where
+    # the oracle's do, and the other subgrid is unaffected
+    if impl:
+        monkeypatch.setenv("IDG_GRIDDER_IMPL", impl)
+        monkeypatch.setenv("IDG_DEGRIDDER_IMPL", impl)
+    st, ts, T, C, G, S = 2, 2, 8, 4, 256, 32
+    a = idg.generate(st, ts, T, C, G, S)
+    p = dict(nr_subgrids=a["metadata"].size, grid_size=G, subgrid_size=S,
+             image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0, nr_channels=C,
+             nr_stations=st)
+    vis = a["visibilities"].copy()
+    vis[0, 3, 1, 2, 0] = bad
+    g = _grid(idg, p, a, vis=vis)
+    go = np.zeros_like(g)
+    oracle_lib.gridder(*_params(p), a["uvw"], a["wavenumbers"], vis,
+                       a["spheroidal"], a["aterms"], a["metadata"], go)
+    assert np.array_equal(np.isfinite(g), np.isfinite(go))
+    assert not np.isfinite(go[0]).any() and np.isfinite(go[1]).all()
+    sg = a["subgrids"].copy()
+    sg[0, 1, 5, 7, 1] = bad
+    d = _degrid(idg, p, a, sg=sg)
+    do = np.zeros_like(d)
+    oracle_lib.degridder(*_params(p), a["uvw"], a["wavenumbers"], do,
+                         a["spheroidal"], a["aterms"], a["metadata"], sg)
+    assert np.array_equal(np.isfinite(d), np.isfinite(do))
+    assert not np.isfinite(do[0]).any() and np.isfinite(do[1]).all()
+
+
 W_SWEEP = [
     (3, 2, 16, 8, 512, 32),
     (2, 1, 9, 7, 256, 24),
