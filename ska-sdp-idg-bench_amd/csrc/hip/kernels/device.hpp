@@ -75,8 +75,13 @@ __device__ __forceinline__ floatx2 tail_k_rev(floatx2 neg_pidx, float kb) {
 // (gridder, S = 32) sums the accumulator tiles into an f32 master every
 // kFlushFills fills (at most 32 K-steps each).
 constexpr int kPrecTail = 1, kPrecFlush = 2, kPrecTailAlt = 4;
+// Every 16 fills (round 5; 8 in round 4): C = 256 gridder 3.35e-6 from the
+// exact sum against 2.74e-6 (the reference's own output: 1.27e-5), its
+// counter traffic 7.90 -> 6.63 GB at NR_TIMESLOTS = 4 (1.49x -> 1.25x the
+// algorithmic bytes); 32 fills (5.97 GB) put a configs[2] sample at 6.98e-6
+// (profiles/r05/flush/).
 #ifndef IDG_FLUSH_FILLS
-#define IDG_FLUSH_FILLS 8
+#define IDG_FLUSH_FILLS 16
 #endif
 constexpr int kFlushFills = IDG_FLUSH_FILLS;
 

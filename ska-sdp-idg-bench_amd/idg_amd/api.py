@@ -461,7 +461,7 @@ def kernel_name(direction, subgrid_size, nr_channels):
 
 
 PRECISION_BITS = {1: "reduction tail on every phasor",
-                  2: "blocked summation (f32 master every 8 fills)",
+                  2: "blocked summation (f32 master every 16 fills)",
                   4: "reduction tail on one channel per quad"}
 
 
