@@ -109,6 +109,9 @@ SWEEP = [
     (2, 1, 700, 2, 1024, 32),   # many timesteps (> 256 degridder units)
     (2, 1, 7, 3, 256, 33),      # odd S: no mirror pairs, single-pixel GEMMs
     (2, 1, 6, 5, 128, 15),      # odd S, S^2 = 225 < one 256-pixel pass
+    (2, 1, 5, 3, 1000, 48),     # S = 48 (runtime S, 1,152 mirror pairs), G = 1000
+    (2, 1, 3, 2, 1024, 128),    # S = 128: 8,192 mirror pairs, several chunks
+    (5, 1, 4, 3, 999, 20),      # odd G, 10 baselines
 ]
 
 

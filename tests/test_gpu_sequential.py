@@ -90,6 +90,8 @@ SWEEP = [
     (2, 1, 7, 3, 256, 33),      # odd S: no mirror pairs
     (2, 1, 6, 5, 128, 15),      # odd S, S^2 < one pixel pass
     (2, 2, 128, 256, 1024, 32), # the -c NR_CHANNELS=256 shape (T x C 32,768)
+    (2, 1, 3, 2, 1024, 128),    # S = 128 (runtime S)
+    (5, 1, 4, 3, 999, 20),      # odd G, 10 baselines
 ]
 
 
