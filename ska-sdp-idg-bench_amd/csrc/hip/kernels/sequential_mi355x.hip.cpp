@@ -6,7 +6,7 @@
 // the complex MAC on the matrix cores in K-blocked f16x2-split GEMMs: closer
 // to the exact sum of the reference's phases than the reference itself, but
 // in a different rounding sequence.  At T x C = 32,768 (BASELINE configs[2])
-// the reference metric puts that 1.37e-5 from the reference's own output
+// the reference metric puts that 1.30e-5 from the reference's own output
 // (DESIGN.md §3.1), because the reference's output is itself 1.27e-5 from
 // exact.  These kernels instead repeat the reference's rounding sequence:
 //
