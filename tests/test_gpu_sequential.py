@@ -203,7 +203,7 @@ def test_reference_harness_sequential_error_zero(exe, env):
     """The reference's own unmodified harness (oracle/_ref, tests/
     {gridder,degridder}_common.cpp) with the sequential kernels: PASSED with
     error 0 -- including -c NR_CHANNELS=256 at the default T = 128, where the
-    default MFMA gridder prints FAILED 1.374e-5."""
+    default MFMA gridder prints FAILED 1.30e-5."""
     path = os.path.join(REF_HARNESS, exe)
     if not os.path.exists(path):
         pytest.skip("oracle/_ref harness not built (needs /root/reference "
