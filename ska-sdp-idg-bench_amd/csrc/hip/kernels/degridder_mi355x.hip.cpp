@@ -48,6 +48,16 @@
 #ifndef IDG_DEGRID_WAVES
 #define IDG_DEGRID_WAVES 4
 #endif
+// A subgrid of several K-chunks (S = 64; the general path of the combined
+// kernel) takes its f16 scale per chunk, from the chunk's own entries, as a
+// single-chunk subgrid does (round 5).  IDG_DEGRID_CHUNK_SCALE=0: one scale
+// per subgrid from a pass over every pixel entry before the first chunk --
+// whose bytes the later chunks then re-read from beyond L2 (configs[4]
+// degridder 29.43 -> 29.0 ms, 11.86 -> 10.08 GB per launch; DESIGN.md
+// §5.000).
+#ifndef IDG_DEGRID_CHUNK_SCALE
+#define IDG_DEGRID_CHUNK_SCALE 1
+#endif
 
 namespace idg_mi355x {
 
@@ -316,7 +326,7 @@ __device__ __forceinline__ void degrid_mfma(
     }
   };
 
-  // Per-subgrid power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range
+  // Per-chunk power-of-two scale: |S|, |D| <= 2 max|P'| stay in f16 range
   // (below 2^IDG_DEGRID_BSCALE: high in the range keeps the split's lo part
   // a normal f16 for all but the smallest pixels).
   auto scale_exp = [](float vmax) {
@@ -324,8 +334,9 @@ __device__ __forceinline__ void degrid_mfma(
     if (vmax > 0.0f && vmax <= 3.0e38f) frexpf(vmax, &e);
     return e;
   };
-  int e;
+  int e = 0;
   static_assert(KP / 2 <= kThreads, "one K-block per thread in a single chunk");
+  constexpr bool kChunkScale = IDG_DEGRID_CHUNK_SCALE != 0;
   if (single) {
     // one chunk: every thread computes its K-block's entries once (NW = 8:
     // the upper half repeats the last K-block, for the max only), the
@@ -340,7 +351,7 @@ __device__ __forceinline__ void degrid_mfma(
     e = scale_exp(2.0f * block_max(v));
     if (has_block) store_block(tid, k, ldexpf(1.0f, IDG_DEGRID_BSCALE - e));
     __syncthreads();
-  } else {
+  } else if constexpr (!kChunkScale) {
     float v = 0.0f;
     for (int p = tid; p < npix; p += kThreads) {
       float4 pa, pb, geo;
@@ -350,11 +361,28 @@ __device__ __forceinline__ void degrid_mfma(
     }
     e = scale_exp(2.0f * block_max(v));
   }
-  const float scale = ldexpf(1.0f, IDG_DEGRID_BSCALE - e),
-              unscale = ldexpf(1.0f, e - IDG_DEGRID_BSCALE);
+  float scale = ldexpf(1.0f, IDG_DEGRID_BSCALE - e),
+        unscale = ldexpf(1.0f, e - IDG_DEGRID_BSCALE);
   // B fragments and geometry of pairs [pc0, pc0 + KP): one thread per
   // K-block (2 pairs), writing all 16 column lanes of it.
   auto build = [&](int pc0) {
+    if constexpr (kChunkScale) {
+      // the chunk's own scale: every thread's K-block entries (the last
+      // K-block again past KP/2, for the maximum only), the workgroup
+      // maximum, then the split -- the single chunk's steps, per chunk
+      Block k;
+      const bool has_block = tid < KP / 2;
+      entries(pc0, has_block ? tid : KP / 2 - 1, k);
+      float v = 0.0f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        v = fmaxf(v, fmaxf(absmax(k.pa[h], k.pb[h]), absmax(k.ma[h], k.mb[h])));
+      const int ec = scale_exp(2.0f * block_max(v));
+      scale = ldexpf(1.0f, IDG_DEGRID_BSCALE - ec);
+      unscale = ldexpf(1.0f, ec - IDG_DEGRID_BSCALE);
+      if (has_block) store_block(tid, k, scale);
+      return;
+    }
     // an opaque copy of tid per call: the addresses derived from it are
     // formed here, not hoisted out of the chunk loop and kept live across
     // the MFMA loops (they were spilled: scratch 92 -> 36 B/lane at S = 32,
