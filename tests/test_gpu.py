@@ -1092,6 +1092,52 @@ def test_s64_mirror_passes_on_four_workgroups_bitwise(idg, wmix,
     assert orc.Oracle().check_error(g, go)[0] <= TOLERANCE
 
 
+@pytest.mark.parametrize("wmix", [False, True])
+def test_s64_degridder_chunks_deterministic_and_vs_oracle(idg, oracle_lib,
+                                                          wmix, monkeypatch):
+    """S = 64 degridder, whose subgrids span several K-chunks, each chunk
+    with its own f16 scale (round 5): the two-kernel form (8-wave mirror
+    kernel, two 1,024-pair chunks; with wmix, every third subgrid w != 0 on
+    the queue-fed general kernel, four 1,024-pixel chunks) and the combined
+    kernel (512-pair / 512-pixel chunks) each give bit-identical
+    visibilities run to run, agree within the parity bar, and match the
+    oracle on sampled subgrids."""
+    import torch
+    st, ts, T, C, G, S = 50, 8, 32, 16, 1024, 64
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    if wmix:
+        a["uvw"][1::3, :, 2] = 41.0
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    assert p["nr_subgrids"] >= 8192  # the two-kernel form
+    dev = _to_device(a)
+    outs = {}
+    for form in ("split", "combined"):
+        monkeypatch.setenv("IDG_KERNEL_FORM", form)
+        runs = [_ddegrid(idg, p, dev, dev["subgrids"]) for _ in range(2)]
+        torch.cuda.synchronize()
+        assert torch.equal(runs[0], runs[1]), form
+        outs[form] = runs[0]
+    ns = p["nr_subgrids"]
+    two, one = outs["split"], outs["combined"]
+    diff = (two.double() - one.double()).reshape(ns, -1).abs().amax(1)
+    mag = one.double().reshape(ns, -1).abs().amax(1)
+    assert float((diff / mag).max()) <= TOLERANCE
+    import oracle as orc
+    for s in (0, 1, ns // 2 + 1, ns - 1):
+        md0 = a["metadata"][s:s + 1].copy()
+        md0["time_offset"] = 0
+        do = np.zeros((1, T, C, 4, 2), np.float32)
+        orc.Oracle().degridder(*_params(dict(p, nr_subgrids=1)),
+                               np.ascontiguousarray(a["uvw"][s]),
+                               a["wavenumbers"], do, a["spheroidal"],
+                               a["aterms"], md0,
+                               np.ascontiguousarray(a["subgrids"][s:s + 1]))
+        d = two[s:s + 1].cpu().numpy()
+        assert orc.Oracle().check_error(d, do)[0] <= TOLERANCE, s
+
+
 def test_workspaces_released_with_their_stream(idg, full_mixed,
                                                monkeypatch):
     """idg_release_workspaces: the split-form launches on a private stream
