@@ -178,16 +178,20 @@ def test_sequential_mirror_fallback_on_mixed_w(idg, oracle_lib, sequential):
 
 @pytest.mark.parametrize("lo,hi,stride", [
     (0, 0x46000000, 3),            # |y| < 2^13: every IDG phase, 1 in 3
+    (0x46000000, 0x47000000, 1),   # [2^13, 2^15): every float (the device's
+                                   # immediate-select table branch; G = 8192)
     (0, 0x7F800000, 61)])          # every finite float class, 1 in 61
 def test_restated_sincosf_on_the_gpu_bit_exact_to_glibc(lo, hi, stride):
     # the device build of csrc/common/sincosf_glibc.hpp (its own table
-    # lookup and int64 -> double conversion) against the host's glibc
+    # lookup and int64 -> double conversion) against the host's glibc, and
+    # the kernels' one-polynomial form sincosf_glibc_dev beside it
     path = os.path.join(REPO, "tests", "harness", "bin", "sincosf_gpu_check")
     assert os.path.exists(path), "build the harness: make -C tests/harness"
     r = subprocess.run([path, hex(lo), hex(hi), str(stride)],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert " mismatch 0" in r.stdout, r.stdout
+    assert " mismatch 0 " in r.stdout, r.stdout
+    assert " mismatch_dev 0" in r.stdout, r.stdout
 
 
 REF_HARNESS = os.path.join(REPO, "oracle", "_ref")
