@@ -1144,7 +1144,13 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * IDG_GRID_NW : kBlock,
 // visibilities from its L2 -- one pass after another in one workgroup
 // re-streamed them from memory each pass (2.0x the algorithmic bytes,
 // profiles/r04/kernels_s64).  Each workgroup forms the same scale from the
-// same first fill, so the output is the one-workgroup kernel's.
+// same first fill, so the output is the one-workgroup kernel's as long as no
+// later fill rescales: in the one-workgroup kernel a rescale in pass q
+// carries into passes q+1.. (the scale e lives across the pass loop), while
+// each split workgroup restarts from the prologue's e.  On data where a late
+// fill grows more than 8x past the first the two forms then differ in their
+// f16 splits, both within the parity bar
+// (tests/test_gpu.py::test_s64_split_forms_with_a_late_loud_timestep).
 template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail,
           int SPLIT = 1>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
@@ -1183,6 +1189,11 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     return;
   }
   constexpr int kPass = NW * 16 * PT;
+  // SPLIT workgroups of kPass base pixels each cover the S_CT subgrid's
+  // S^2/2 base pixels exactly once, none of them idle
+  static_assert(SPLIT == 1 || (S_CT > 0 && SPLIT * kPass >= S_CT * S_CT / 2 &&
+                               (SPLIT - 1) * kPass < S_CT * S_CT / 2),
+                "mirror_split(S) does not match the pass size");
   grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,

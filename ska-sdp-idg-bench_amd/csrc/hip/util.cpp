@@ -237,10 +237,14 @@ int precision_for(Direction dir, const Problem &p) {
   // over channels; measured 1.00e-6 vs 0.97e-6 from exact at the -c
   // defaults, 8.1e-7 vs 6.7e-7 at C = 256, for 5 % of its time)
   if (dir == Direction::kDegridder) return 0;
-  // the one-channel-per-quad tail cancels only over whole channel quads:
-  // with a partial last quad the every-phasor tail instead
-  const int tail = p.nr_channels % 4 == 0 ? kPrecTailAlt : kPrecTail;
-  return tail | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
+  // gridder: the reduction tail on every phasor.  The one-channel-per-quad
+  // tail (kPrecTailAlt, IDG_PREC=4: a quarter of the adds) cancels only
+  // where a quad's four terms are coherent; on channel-incoherent
+  // visibilities it left the gridder farther from exact than the reference's
+  // own f32 sum (round 5: 1.31e-6 against 0.79e-6 at C = 16,
+  // tests/test_gpu_accuracy.py::test_tail_patterns_on_channel_incoherent_
+  // visibilities), so it is no longer the default
+  return kPrecTail | (p.nr_channels > kTailMinChannels ? kPrecFlush : 0);
 }
 
 std::string validate(const Problem &p, const Extents &e,
@@ -406,7 +410,7 @@ hipError_t release_workspaces(hipStream_t stream, bool all) {
   hipError_t err = hipGetDevice(&dev);
   if (err != hipSuccess) return err;
   std::lock_guard<std::mutex> lock(g_ws_mu);
-  bool freed = false, busy = false;
+  bool busy = false;
   for (auto it = g_ws.begin(); it != g_ws.end();) {
     if (std::get<0>(it->first) != dev ||
         (!all && std::get<1>(it->first) != stream)) {
@@ -418,18 +422,17 @@ hipError_t release_workspaces(hipStream_t stream, bool all) {
       ++it;
       continue;
     }
-    // freed on the null stream (the owning stream may be about to go), then
-    // waited for, so the memory is gone when this returns
+    // freed on the owning stream, so the free is ordered after every kernel
+    // still queued there that uses the slot (torch streams do not
+    // synchronise with the null stream), then that stream is waited for, so
+    // the memory is gone when this returns
     if (it->second.ptr) {
-      const hipError_t e = hipFreeAsync(it->second.ptr, nullptr);
+      const hipStream_t owner = std::get<1>(it->first);
+      hipError_t e = hipFreeAsync(it->second.ptr, owner);
+      if (e == hipSuccess) e = hipStreamSynchronize(owner);
       if (e != hipSuccess && err == hipSuccess) err = e;
-      freed = true;
     }
     it = g_ws.erase(it);
-  }
-  if (freed) {
-    const hipError_t e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess && err == hipSuccess) err = e;
   }
   if (err == hipSuccess && busy) err = hipErrorNotReady;
   return err;

@@ -193,7 +193,9 @@ bool two_kernel_form(int nr_subgrids);
 
 // Precision options (device.hpp kPrecTail | kPrecFlush | kPrecTailAlt) of
 // the MFMA kernels for a launch: the gridder takes
-// the reduction tail on one channel per quad (kPrecTailAlt) and, above
+// the reduction tail on every phasor (kPrecTail; round 6, was kPrecTailAlt,
+// one channel per quad, until channel-incoherent data showed it losing to the
+// reference's own f32 sum) and, above
 // kTailMinChannels channels, blocked summation (kPrecFlush: C = 256 gridder
 // 8.4e-6 -> 2.0e-6 from exact accumulation); the degridder no tail.
 // IDG_PREC=<0..7> forces the bits for both directions (A/B, tests).

@@ -501,6 +501,8 @@ def release_workspaces(stream=None, all_streams=False):
     import torch
     if all_streams:
         handle = ctypes.c_void_p(None)
+        # every stream's queued launches finished before their slots go
+        torch.cuda.synchronize()
     else:
         handle = _stream_handle(stream)
         (stream or torch.cuda.current_stream()).synchronize()

@@ -1092,6 +1092,44 @@ def test_s64_mirror_passes_on_four_workgroups_bitwise(idg, wmix,
     assert orc.Oracle().check_error(g, go)[0] <= TOLERANCE
 
 
+def test_s64_split_forms_with_a_late_loud_timestep(idg, monkeypatch):
+    """The S = 64 split form is the combined kernel bit for bit only while
+    no fill rescales (gridder_mi355x.hip.cpp, kernel_gridder_mirror_mi355x):
+    with every subgrid's last timestep 64x louder than the rest, a late fill
+    outgrows the first fill's scale.  The two forms then need not be equal
+    bitwise, but both stay within the parity bar of each other and of the
+    oracle on sampled subgrids."""
+    import torch
+    import oracle as orc
+    st, ts, T, C, G, S = 50, 8, 32, 16, 1024, 64
+    a = idg.generate(st, ts, T, C, G, S, nthreads=16)
+    a["visibilities"][:, T - 1] *= 64.0
+    p = dict(nr_subgrids=idg.nr_subgrids_for(st, ts), grid_size=G,
+             subgrid_size=S, image_size=idg.IMAGE_SIZE, w_step_in_lambda=0.0,
+             nr_channels=C, nr_stations=st)
+    assert p["nr_subgrids"] >= 8192  # the two-kernel form
+    dev = _to_device(a)
+    outs = {}
+    for form in ("split", "combined"):
+        monkeypatch.setenv("IDG_KERNEL_FORM", form)
+        outs[form] = _dgrid(idg, p, dev, dev["visibilities"])
+    torch.cuda.synchronize()
+    o = orc.Oracle()
+    for s in (0, p["nr_subgrids"] // 2, p["nr_subgrids"] - 1):
+        split = outs["split"][s:s + 1].cpu().numpy()
+        comb = outs["combined"][s:s + 1].cpu().numpy()
+        assert o.check_error(split, comb)[0] <= TOLERANCE
+        go = np.zeros((1, 4, S, S, 2), np.float32)
+        md0 = a["metadata"][s:s + 1].copy()
+        md0["time_offset"] = 0
+        o.gridder(*_params(dict(p, nr_subgrids=1)),
+                  np.ascontiguousarray(a["uvw"][s]), a["wavenumbers"],
+                  np.ascontiguousarray(a["visibilities"][s]),
+                  a["spheroidal"], a["aterms"], md0, go)
+        for got in (split, comb):
+            assert o.check_error(got, go)[0] <= TOLERANCE
+
+
 @pytest.mark.parametrize("wmix", [False, True])
 def test_s64_degridder_chunks_deterministic_and_vs_oracle(idg, oracle_lib,
                                                           wmix, monkeypatch):

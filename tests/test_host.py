@@ -161,20 +161,26 @@ def test_kernel_selection_names():
 
 
 def test_precision_options_defaults_and_override(monkeypatch):
-    # util.cpp precision_for: gridder tail on one channel per quad, blocked
-    # summation above 16 channels; degridder neither; IDG_PREC overrides
+    # util.cpp precision_for: gridder tail on every phasor (round 6; the
+    # one-channel-per-quad tail lost to the reference's own f32 sum on
+    # channel-incoherent data), blocked summation above 16 channels;
+    # degridder neither; IDG_PREC overrides
     monkeypatch.delenv("IDG_PREC", raising=False)
     assert idg_amd.precision_options("gridder", 32, 16) == (
-        4, "reduction tail on one channel per quad")
+        1, "reduction tail on every phasor")
     bits, desc = idg_amd.precision_options("gridder", 32, 256)
-    assert bits == 6 and "blocked summation" in desc
+    assert bits == 3 and "blocked summation" in desc
     assert idg_amd.precision_options("degridder", 32, 256) == (0, "none")
     # what is built: no blocked summation off S = 32 ...
-    assert idg_amd.precision_options("gridder", 64, 256)[0] == 4
-    # ... the every-phasor tail where the channels end in a partial quad ...
+    assert idg_amd.precision_options("gridder", 64, 256)[0] == 1
+    # ... the same tail whether or not the channels end in a partial quad
     assert idg_amd.precision_options("gridder", 32, 15)[0] == 1
-    assert idg_amd.precision_options("gridder", 32, 300)[0] == 6
+    assert idg_amd.precision_options("gridder", 32, 300)[0] == 3
     assert idg_amd.precision_options("gridder", 32, 301)[0] == 3
+    # the one-channel-per-quad tail stays selectable
+    monkeypatch.setenv("IDG_PREC", "4")
+    assert idg_amd.precision_options("gridder", 32, 16) == (
+        4, "reduction tail on one channel per quad")
     # ... and the alternating tail alone when both tails are asked for
     monkeypatch.setenv("IDG_PREC", "5")
     assert idg_amd.precision_options("gridder", 32, 16)[0] == 4
@@ -280,11 +286,14 @@ SINCOSF_CHECK = os.path.join(REPO, "tests", "harness", "bin", "sincosf_check")
 @pytest.mark.skipif(not os.path.exists(SINCOSF_CHECK),
                     reason="tests/harness not built (make -C tests/harness)")
 @pytest.mark.parametrize("lo,hi,stride", [
-    # every float of magnitude below 2^13 (all IDG phases: |phase| < 3.4e3)
-    (0, 0x46000000, 1),
+    # every float of magnitude below 2^15: the benchmark's phases (|phase| <
+    # 3.4e3) and the G = 8192 parity cases' (about pi * G / 2 per axis, up
+    # to 1e4 and more), i.e. the whole range the device serves from the
+    # immediate-select branch of sincosf_large (table entries 0 and 1)
+    (0, 0x47000000, 1),
     # every 61st finite float beyond (the large-argument reduction's other
     # table entries, inf/nan excluded)
-    (0x46000000, 0x7F800000, 61)])
+    (0x47000000, 0x7F800000, 61)])
 def test_restated_sincosf_bit_exact_to_glibc(lo, hi, stride):
     """csrc/common/sincosf_glibc.hpp, the phasor of the sequential kernels,
     computes glibc's sincosf bit for bit (both signs), and sincosf is exactly

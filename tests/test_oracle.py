@@ -244,7 +244,9 @@ def test_reduction_tail_on_one_channel_per_quad_emulated(C):
     """The gridder's phase-reduction tail, emulated exactly with double sums
     (tests/emul/tail_mean_emul.py): without it the
     coherent sums keep a systematic phase error; added as 4c to the first
-    channel of every quad (kPrecTailAlt, the shipped gridder) it is as close
+    channel of every quad (kPrecTailAlt, IDG_PREC=4; the default until
+    round 5, when channel-incoherent data showed it losing to the
+    reference's own sum, tests/test_gpu_accuracy.py) it is as close
     to the exact sum as the every-phasor add within 2x, and at least 4x
     closer than none -- while a per-quad pattern or one channel in 16 is
     worse than one in 4."""
