@@ -30,6 +30,15 @@ cpu_baseline times the reference's own CPU path (oracle/_ref) on a bounded
 sample of the same batch, on the host cores this process may use and on one
 thread as the reference builds it.
 
+Beside `value` (never in it), a one-GPU default run also times: the `wterm`
+batch; the bit-exact order-preserving kernels (`sequential`, with their own
+issue-model roofline, and `sequential.configs2`: configs[2] at NR_TIMESLOTS=4
+with the order-preserving gridder); and BASELINE configs[2] (`configs2`, C =
+256 at NR_TIMESLOTS=4) and configs[4] (`configs4`, S = 64, the full batch) on
+the default kernels, each with its roofline, counter traffic and issue
+efficiency priced from the committed profile of the same launch
+(profiles/traffic.json).
+
     python bench.py [--gpus N --steps K --warmup W] [--workload default]
                     [--mode sharded|replicated] [--dump DIR]
 
@@ -143,6 +152,10 @@ def parse(argv=None):
                          "wterm batch and the sequential kernels; profiling "
                          "runs pass it so only the headline launches are "
                          "counted)")
+    ap.add_argument("--no-workload-legs", action="store_true",
+                    help="skip the configs[2] / configs[4] side legs of a "
+                         "one-GPU default run (the wterm and sequential "
+                         "legs still run)")
     ap.add_argument("--dump", default=None,
                     help="rank 0 writes the gathered gridder subgrids, "
                          "degridded visibilities and summed uv grid here "
@@ -504,6 +517,117 @@ def roofline_for(entry, kernel, flops, nvis, t, nsub_launch, nsub_profiled,
     return out
 
 
+def roofline_seq(entry, kernel, flops, nvis, t, nsub_launch):
+    """Roofline of an order-preserving (bit-exact) kernel:
+    it repeats the reference's own arithmetic -- glibc's sincosf in f64 per
+    phasor, f32 sums in the reference's order -- so its floor is the issue
+    time of that instruction stream, not a tensor or transcendental unit:
+        t_issue = sum over VALU classes (SQ counters) of count x measured
+                  issue cost / 1024 SIMDs / 2.4 GHz
+    (tools/probes/summarize_seq.py, the costs from
+    tools/probes/seq_rates_probe.hip), frac = t_issue / t, achieved = the
+    reference work model's FLOPs / t, peak = the same FLOPs / t_issue."""
+    achieved = flops / t / 1e12
+    out = {"bound": "valu-issue", "achieved": round(achieved, 3),
+           "unit": "TFLOP/s", "kernel": kernel,
+           "resource": "VALU issue of the kernel's own instruction stream "
+                       "(glibc sincosf restated in f64, sums in the "
+                       "reference's order)"}
+    im = (entry or {}).get("issue_model")
+    if im:
+        scale = nsub_launch / entry.get("nr_subgrids", nsub_launch)
+        t_issue = im["t_issue_ms"] / 1e3 * scale
+        out.update({
+            "peak": round(flops / t_issue / 1e12, 3),
+            "frac": round(t_issue / t, 4),
+            "t_issue_ms": round(t_issue * 1e3, 4),
+            "valu_mix_per_launch": {k: int(v * scale) for k, v in
+                                    im.get("valu_mix", {}).items()},
+            "costs": im.get("costs"), "source": im.get("source"),
+            "note": "class counts x measured issue cost / 1024 SIMDs / "
+                    "2.4 GHz over the measured time (the SQ profile's "
+                    "launch, scaled to this one's subgrids)"})
+    else:
+        out.update({"peak": None, "frac": None,
+                    "note": "no committed SQ profile for this kernel"})
+    out["fp32_equivalent"] = {
+        "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+        "ratio": round(achieved / FP32_PEAK_TFLOPS, 4)}
+    return out
+
+
+def algorithmic_bytes(w, nsub):
+    """Bytes a launch must move at least: the visibilities once, the subgrids
+    once, the uvw rows once (the A-terms and taper are L2-resident)."""
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+    return nsub * T * C * 32 + nsub * 4 * S * S * 8 + nsub * T * 12
+
+
+def time_workload(args, name, timeslots, stream, dist, steps, impl=None,
+                  batch=None):
+    """One of BASELINE.json's other single-GPU configs, timed beside `value`
+    (never in it): its own batch from the reference generators (a timeslot
+    subset where stated), the same timed step, per-kernel figures and the
+    dominant kernel's roofline priced from the committed profile of the
+    same launch (profiles/traffic.json[name]).  impl: IDG_GRIDDER_IMPL for
+    the leg (e.g. "sequential").  Returns (leg, batch) so a second leg can
+    reuse the batch."""
+    import torch
+    import idg_amd
+    w = workload(name, timeslots)
+    T, C, S = w["nr_timesteps"], w["nr_channels"], w["subgrid_size"]
+    if batch is None:
+        progress(f"side leg {name}: generating the batch")
+        a = make_batch(w, nthreads=16)
+        batch = (a, upload(shard_batch(a, 0, 1)))
+    a, dev = batch
+    nsub = int(a["metadata"].size)
+    nvis = nsub * T * C
+    saved = os.environ.get("IDG_GRIDDER_IMPL")
+    if impl:
+        os.environ["IDG_GRIDDER_IMPL"] = impl
+    try:
+        names = {d: idg_amd.kernel_name(d, S, C)
+                 for d in ("gridder", "degridder")}
+        el, tg, td, _, _, _ = time_steps(w, dev, nsub, steps, 1, stream,
+                                         dist, min_warmup_s=0.5)
+    finally:
+        if saved is None:
+            os.environ.pop("IDG_GRIDDER_IMPL", None)
+        else:
+            os.environ["IDG_GRIDDER_IMPL"] = saved
+    flops = idg_amd.flops_gridder(C, nsub * T, nsub, S)
+    times = {"gridder": tg, "degridder": td}
+    dom = "gridder" if tg >= td else "degridder"
+    entry = profile_entry(args.traffic_file, name, names[dom])
+    if "sequential" in names[dom]:
+        rl = roofline_seq(entry, names[dom], flops, nvis, times[dom], nsub)
+    else:
+        rl = roofline_for(entry, names[dom], flops, nvis, times[dom], nsub,
+                          (entry or {}).get("nr_subgrids", nsub), w)
+    rl["algorithmic_bytes"] = algorithmic_bytes(w, nsub)
+    if rl.get("traffic"):
+        rl["traffic_over_algorithmic"] = round(
+            rl["traffic"] / rl["algorithmic_bytes"], 3)
+    leg = {
+        "value": round(nvis / (el / steps) / 1e6, 2), "unit": "Mvis/s",
+        "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
+        "kernels": {d: {"kernel": names[d], "ms": round(times[d] * 1e3, 4),
+                        "mvis_s": round(nvis / times[d] / 1e6, 2)}
+                    for d in names},
+        "baseline_config": BASELINE_CONFIG[name],
+        "workload": (f"{name}: NR_STATIONS={w['nr_stations']} "
+                     f"NR_TIMESLOTS={w['nr_timeslots']} "
+                     f"NR_TIMESTEPS_SUBGRID={T} NR_CHANNELS={C} "
+                     f"SUBGRID_SIZE={S} GRID_SIZE={w['grid_size']}: "
+                     f"{nsub} subgrids, {nvis} visibilities"),
+        "roofline": rl,
+    }
+    if entry and entry.get("source"):
+        leg["traffic_source"] = entry["source"]
+    return leg, batch
+
+
 # ---------------------------------------------------------------------------
 # Side legs of a one-GPU default run (beside `value`, never in it)
 # ---------------------------------------------------------------------------
@@ -574,6 +698,8 @@ def time_side_legs(args, w, a, dev, nsub, stream, dist, value):
             else:
                 os.environ[k] = v
     qv = nvis / (el / qsteps) / 1e6
+    flops = idg_amd.flops_gridder(C, nsub * T, nsub, S)
+    qdom = "gridder" if tg >= td else "degridder"
     side["sequential"] = {
         "value": round(qv, 2), "unit": "Mvis/s", "steps": qsteps,
         "ms_per_step": round(el / qsteps * 1e3, 4),
@@ -581,10 +707,48 @@ def time_side_legs(args, w, a, dev, nsub, stream, dist, value):
         "gridder_mvis_s": round(nvis / tg / 1e6, 2),
         "degridder_mvis_s": round(nvis / td / 1e6, 2),
         "kernels": names_q, "slowdown_vs_value": round(value / qv, 2),
+        "roofline": roofline_seq(
+            profile_entry(args.traffic_file, "default", names_q[qdom]),
+            names_q[qdom], flops, nvis, max(tg, td), nsub),
+        "roofline_other": roofline_seq(
+            profile_entry(args.traffic_file, "default",
+                          names_q["degridder" if qdom == "gridder"
+                                  else "gridder"]),
+            names_q["degridder" if qdom == "gridder" else "gridder"], flops,
+            nvis, min(tg, td), nsub),
         "note": "IDG_{GRIDDER,DEGRIDDER}_IMPL=sequential: the reference CPU "
                 "path's rounding sequence (glibc sincosf restated, t-then-c "
                 "f32 sums per pixel; y-then-x per visibility), bit-exact to "
                 "app/CPU (tests/test_gpu_sequential.py); beside `value`"}
+    if args.no_workload_legs:
+        return side
+    # -- BASELINE configs[2] and configs[4] on the default (MFMA) kernels, and
+    #    configs[2] with the order-preserving gridder -- the mode that keeps
+    #    the reference's own rounding at T x C = 32,768 --
+    #    beside the default degridder, which meets the reference metric there
+    wsteps = max(1, min(args.steps, 3))
+    side["configs2"], batch = time_workload(args, "c256", 4, stream, dist,
+                                            wsteps)
+    side["configs2"]["note"] = ("BASELINE configs[2] (C = 256) at "
+                                "NR_TIMESLOTS=4 (a fifth of the batch); "
+                                "beside `value`, not in it")
+    seq2, _ = time_workload(args, "c256", 4, stream, dist, 1,
+                            impl="sequential", batch=batch)
+    seq2["note"] = ("configs[2] at NR_TIMESLOTS=4 with the order-preserving "
+                    "gridder (bit-exact to app/CPU) and the default "
+                    "degridder (within the reference metric of app/CPU at "
+                    "every config): the configuration that prints PASSED "
+                    "under the reference's own harness at T x C = 32,768")
+    side["sequential"]["configs2"] = seq2
+    del batch, _
+    torch.cuda.empty_cache()
+    side["configs4"], batch = time_workload(args, "s64", None, stream, dist,
+                                            wsteps)
+    side["configs4"]["note"] = ("BASELINE configs[4] (S = 64, A-term + "
+                                "spheroidal), the full batch; beside "
+                                "`value`, not in it")
+    del batch
+    torch.cuda.empty_cache()
     return side
 
 
@@ -1050,7 +1214,8 @@ def main(argv=None):
     side = None
     if (world == 1 and args.workload == "default" and not args.no_side and
             not args.dump):
-        progress("side legs (wterm batch, sequential kernels)")
+        progress("side legs (wterm batch, sequential kernels, configs[2] "
+                 "and configs[4])")
         side = time_side_legs(args, w, a, dev, nsub, stream, dist,
                               nvis_job / sec_per_step / 1e6)
 
@@ -1105,6 +1270,8 @@ def main(argv=None):
             if world == 1 else None),
         "wterm": side["wterm"] if side else None,
         "sequential": side["sequential"] if side else None,
+        "configs2": side.get("configs2") if side else None,
+        "configs4": side.get("configs4") if side else None,
         "cpu_baseline": None,
     }
     t_cpu = 0.0
