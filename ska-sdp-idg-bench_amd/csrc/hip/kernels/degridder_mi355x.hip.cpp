@@ -207,8 +207,15 @@ __device__ __forceinline__ floatx2 phase_rev_bcast(floatx2 p, floatx2 kp,
 }
 static_assert(kInv2PiHi == 0.15915494f, "phase_rev_bcast's inline constant");
 
+// KS: K split -- the workgroup's waves form KS groups of NW / KS waves;
+// every group covers all timesteps and channel tiles, each over its own
+// share of the chunk's K-steps (KS = 2: the 16-wave S = 64 mirror kernel,
+// whose eight timestep waves would otherwise leave half the workgroup idle
+// at T = 128).  Group 1 stores its partial sums, the workgroup barrier
+// orders them (same CU: one L1), group 0 adds its own on top: p1 + p0, the
+// same float as the two-chunk form's p0 + p1 (two-term addition commutes).
 template <int S_CT, int CT, int CB, int KP, bool MIRROR, int NW,
-          bool TAIL = true>
+          bool TAIL = true, int KS = 1>
 __device__ __forceinline__ void degrid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -229,6 +236,9 @@ __device__ __forceinline__ void degrid_mfma(
   if constexpr (!MIRROR) asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
+  static_assert(NW % KS == 0 && KS <= 2, "whole wave groups per K group");
+  constexpr int kTWaves = NW / KS;  // waves per timestep pass
+  const int wave_t = wave % kTWaves, wave_k = wave / kTWaves;
   // MIRROR: K runs over pixel pairs (b, npix-1-b); general: over single
   // pixels, as pairs whose mirror term is zero (S = D = P'), w-term on.
   const int half = MIRROR ? npix / 2 : npix;
@@ -406,8 +416,9 @@ __device__ __forceinline__ void degrid_mfma(
       build(pc0);
       __syncthreads();
     }
-    for (int t0 = 0; t0 < nt; t0 += 16 * NW) {  // NW waves x 16 timesteps
-      const int t_row = t0 + wave * 16 + col;  // this lane's A row timestep
+    // kTWaves waves x 16 timesteps per pass
+    for (int t0 = 0; t0 < nt; t0 += 16 * kTWaves) {
+      const int t_row = t0 + wave_t * 16 + col;  // this lane's A row timestep
       const idg::UVWCoordinate<float> c =
           uvw[g.time_offset + min(t_row, nt - 1)];
       for (int cg0 = 0; cg0 < C; cg0 += CT) {
@@ -419,7 +430,10 @@ __device__ __forceinline__ void degrid_mfma(
         for (int j = 0; j < CT; ++j) acc[j] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
         {
         const int nks = (min(KP, half - pc0) + 7) / 8;
-        for (int ks = 0; ks < nks; ++ks) {
+        // this wave's K group's K-steps
+        const int ks_per = (nks + KS - 1) / KS;
+        const int ks_end = min(nks, (wave_k + 1) * ks_per);
+        for (int ks = wave_k * ks_per; ks < ks_end; ++ks) {
           const int pp = 8 * ks + 2 * grp;
           const float2 gl = *reinterpret_cast<const float2 *>(geo_l + pp);
           const float2 gm = *reinterpret_cast<const float2 *>(geo_m + pp);
@@ -480,10 +494,11 @@ __device__ __forceinline__ void degrid_mfma(
       // channel j's, lanes col >= 8 channel j+1's, and each 16-lane group
       // writes the two adjacent 32-byte visibilities (t, j), (t, j+1) as one
       // contiguous 64-byte store -- no LDS shuffle, no inactive lanes.
-      const bool full_tc = t0 + 16 * NW <= nt && cg0 + CT <= C;
+      const bool full_tc = t0 + 16 * kTWaves <= nt && cg0 + CT <= C;
+      auto store = [&](bool add) {
       if (full_tc) {
         float *vrow = reinterpret_cast<float *>(visibilities) +
-                      (static_cast<size_t>(g.time_offset + t0 + wave * 16 +
+                      (static_cast<size_t>(g.time_offset + t0 + wave_t * 16 +
                                            grp * 4) * C + cg0) * 8 + col;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -494,7 +509,7 @@ __device__ __forceinline__ void degrid_mfma(
             const float s0 = v0 + row_ror8(v0);
             const float s1 = v1 + row_ror8(v1);
             const float out = (col < 8 ? s0 : s1) * unscale;
-            if (pc0 == 0)
+            if (!add)
               dst[8 * j] = out;
             else
               dst[8 * j] += out;
@@ -508,15 +523,24 @@ __device__ __forceinline__ void degrid_mfma(
         for (int r = 0; r < 4; ++r) {
           const float v = acc[j][r];
           const float other = __shfl_xor(v, 8);
-          const int t = t0 + wave * 16 + grp * 4 + r;
+          const int t = t0 + wave_t * 16 + grp * 4 + r;
           if (col < 8 && t < nt && ch < C) {
             float *dst = reinterpret_cast<float *>(
                 visibilities + ((g.time_offset + t) * C + ch) * 4);
             const float out = (v + other) * unscale;
-            dst[col] = pc0 == 0 ? out : dst[col] + out;
+            dst[col] = !add ? out : dst[col] + out;
           }
         }
       }
+      }
+      };
+      if constexpr (KS == 1) {
+        store(pc0 != 0);
+      } else {
+        // group 1's partial sums first, then group 0's added on top
+        if (wave_k == 1) store(pc0 != 0);
+        __syncthreads();
+        if (wave_k == 0) store(true);
       }
     }
   }
@@ -724,7 +748,14 @@ __global__ void __launch_bounds__(MODE == 1 ? 64 * NW : kBlock,
 #endif
 constexpr int mirror_kp64() { return IDG_DEGRID_KP64; }
 
-template <int S_CT, int CT, int NW, bool TAIL = true>
+// KPX > 0: pairs per chunk (else as below); KS: K split (degrid_mfma).
+// The S = 64 single-chunk form (round 6): KPX = 2,048 -- the whole
+// subgrid's pairs, 160 KB of LDS, one 16-wave workgroup per CU in two K
+// groups of 8 waves -- so the visibilities are written once
+// instead of written, read back and written again (the two-chunk form's
+// 2.08x the algorithmic bytes, profiles/r05/kernels_s64).
+template <int S_CT, int CT, int NW, bool TAIL = true, int KPX = 0,
+          int KS = 1>
 __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
     kernel_degridder_mirror_mi355x(
         const int grid_size, int subgrid_size, float image_size,
@@ -741,7 +772,8 @@ __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
   // four, and its visibilities are written, read back and written again
   // once instead of three times (profiles/r04/kernels_s64: 18.7 GB per
   // launch against 4.85 GB algorithmic)
-  constexpr int KP = (S_CT == 64 && NW == 8) ? mirror_kp64() : 512;
+  constexpr int KP =
+      KPX > 0 ? KPX : (S_CT == 64 && NW == 8) ? mirror_kp64() : 512;
   __shared__ unsigned lds[DegridMfmaLds<KP>::kWords];
   const int S = S_CT > 0 ? S_CT : subgrid_size;
   const int npix = S * S;
@@ -763,10 +795,26 @@ __global__ void __launch_bounds__(64 * NW, IDG_DEGRID_WAVES)
     if (tid == 0) queue_push(queue, gridDim.x, s);
     return;
   }
-  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW, TAIL>(
+  degrid_mfma<S_CT, CT, IDG_DEGRID_CB, KP, true, NW, TAIL, KS>(
       g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
       visibilities, spheroidal, aterms,
       subgrids + static_cast<size_t>(s) * 4 * npix, lds);
+}
+
+// IDG_DEGRID_S64=1: the S = 64 mirror kernel of the two-kernel form in the
+// single-chunk form above; 2 (default): the two-chunk form (8 waves,
+// 1,024-pair chunks).  Measured on one box (profiles/r06/s64_single/): the
+// single chunk moves 7.01 GB per launch against 10.09 (5.23 GB with the
+// channel groups split instead of K, at 33.7 ms) but runs 32.5 ms against
+// 29.3: with one workgroup per CU nothing overlaps its chunk build and the
+// partial-sum hand-over, which the two-chunk form's second workgroup hides.
+#ifndef IDG_DEGRID_S64
+#define IDG_DEGRID_S64 2
+#endif
+template <bool TAIL>
+const void *degridder_mirror_s64_single() {
+  return reinterpret_cast<const void *>(
+      &kernel_degridder_mirror_mi355x<64, IDG_DEGRID_CT, 16, TAIL, 2048, 2>);
 }
 
 template <int S_CT, int CT, bool TAIL = true>
@@ -931,7 +979,11 @@ KernelChoice select_degridder(const Problem &p) {
     if (IDG_DEGRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
       // mirror-eligible subgrids (even S only), then the others on 8-wave
       // workgroups with 1,024-pixel chunks
-      if (s64 && mirror_kp64() > 512)  // 8 waves, 1,024-pair chunks
+      if (s64 && IDG_DEGRID_S64 == 1)  // 16 waves, one 2,048-pair chunk
+        k.parts[0] = {tail ? degridder_mirror_s64_single<true>()
+                           : degridder_mirror_s64_single<false>(),
+                      1024, KernelChoice::kMirror};
+      else if (s64 && mirror_kp64() > 512)  // 8 waves, 1,024-pair chunks
         k.parts[0] = {degridder_set_for<64>(true, tail).mirror, 512,
                       KernelChoice::kMirror};
       else if (p.subgrid_size % 2 == 0)

@@ -155,6 +155,11 @@ def main():
     ap.add_argument("--pmc", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--workload", default="default")
+    ap.add_argument("--nr-subgrids", type=int, default=None,
+                    help="subgrids of the profiled launch (bench.py scales "
+                         "the per-launch figures to its own launch by it)")
+    ap.add_argument("--note", default=None,
+                    help="the profiled workload, stored with each entry")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles",
                                                       "traffic.json"))
     args = ap.parse_args()
@@ -266,6 +271,10 @@ def main():
         if issue:
             entry["issue_bound"] = issue
         entry["mean_ms_under_rocprof"] = round(st["mean_ns"] / 1e6, 4)
+        if args.nr_subgrids:
+            entry["nr_subgrids"] = args.nr_subgrids
+        if args.note:
+            entry["workload"] = args.note
         lines.append(
             f"{n:28s} {st['launches']:8d} {st['mean_ns'] / 1e6:9.4f} "
             f"{st['min_ns'] / 1e6:8.4f} {st['max_ns'] / 1e6:8.4f} "
