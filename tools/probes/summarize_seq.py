@@ -77,8 +77,16 @@ def main():
                     "this traffic.json (bench.py reads it)")
     ap.add_argument("--workload", default="default")
     ap.add_argument("--note", default=None)
+    ap.add_argument("--nr-subgrids", type=int, default=None,
+                    help="subgrids of the profiled launch (bench.py scales "
+                         "the issue model to its own launch by it)")
     ap.add_argument("--frac-int32-quarter", type=float, default=0.35)
-    ap.add_argument("--frac-f32-packed", type=float, default=0.75)
+    ap.add_argument("--frac-f32-packed", type=float, default=None,
+                    help="override both kernels' packed share of the f32 "
+                         "class (default: gridder 0.9 -- per mirror pair "
+                         "20 packed MAC ops beside 2 plain phase FMAs --, "
+                         "degridder 0.75 -- per phasor 12 packed beside 4 "
+                         "plain: phase_index and phase)")
     args = ap.parse_args()
     dur = defaultdict(list)
     for db in glob.glob(os.path.join(args.dir, "ktrace", "**", "*.db"),
@@ -120,7 +128,10 @@ def main():
                                             "SQ_INSTS_VALU_MUL_F32"))
             trans = c.get("SQ_INSTS_VALU_TRANS_F32", 0)
             other = c["SQ_INSTS_VALU"] - f64 - cvt - i32 - i64 - f32 - trans
-            q, pk = args.frac_int32_quarter, args.frac_f32_packed
+            q = args.frac_int32_quarter
+            pk = args.frac_f32_packed
+            if pk is None:
+                pk = 0.9 if k.startswith("gridder") else 0.75
             cyc = (f64 * COST["f64"] + cvt * COST["cvt"] +
                    i32 * (q * COST["int32_quarter"] +
                           (1 - q) * COST["int32_plain"]) +
@@ -164,6 +175,8 @@ def main():
                         "mean_ms_under_rocprof": e["mean_ms"]})
             if args.note:
                 ent["workload"] = args.note
+            if args.nr_subgrids:
+                ent["nr_subgrids"] = args.nr_subgrids
         with open(args.traffic, "w") as f:
             json.dump(tj, f, indent=1)
     print(text)
