@@ -804,10 +804,15 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
     grid_out = torch.empty_like(dev["subgrids"])
     degrid_out = torch.empty_like(dev["visibilities"])
 
+    # ev = (start, middle, end) of a timed step; consecutive steps share
+    # their boundary event (step k's end is step k+1's start), so a step
+    # records two events, not three (each event record costs the stream
+    # ~3.5 us: 3,062 subgrids at N = 8, 1.9527 / 1.9577 / 1.9641 ms per step
+    # with 0 / 2 / 3 events, tools/debug/event_cost.py, profiles/r06/n8/)
     def step(ev=None):
         if nsub == 0:
             return
-        if ev:
+        if ev and ev[0] is not None:
             ev[0].record(stream)
         idg_amd.gridder_launch(*p, dev["uvw"], dev["wavenumbers"],
                                dev["visibilities"], dev["spheroidal"],
@@ -822,8 +827,12 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
         if ev:
             ev[2].record(stream)
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
-              for _ in range(steps)]
+    marks = [torch.cuda.Event(enable_timing=True)
+             for _ in range(2 * steps + 1)]
+    events = [(marks[2 * k] if k == 0 else None, marks[2 * k + 1],
+               marks[2 * k + 2]) for k in range(steps)]
+    bounds = [(marks[2 * k], marks[2 * k + 1], marks[2 * k + 2])
+              for k in range(steps)]
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -861,8 +870,8 @@ def time_steps(w, dev, nsub, steps, warmup, stream, dist, meter=None,
     joules = meter.stop() if meter else None
     elapsed_max = dist.max_over_ranks(elapsed)
     if nsub:
-        t_grid = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
-        t_degrid = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
+        t_grid = sum(e[0].elapsed_time(e[1]) for e in bounds) / steps / 1e3
+        t_degrid = sum(e[1].elapsed_time(e[2]) for e in bounds) / steps / 1e3
     else:
         t_grid = t_degrid = 0.0
     return (elapsed_max, dist.max_over_ranks(t_grid),

@@ -171,8 +171,10 @@ __device__ __forceinline__ int xcd_subgrid(int orig, int nwg) {
 // are zero before a launch pair: zeroed when the workspace is allocated, and
 // zeroed again by the general kernel's last workgroup to finish
 // (queue_retire), so a workspace cached per stream needs no clear per launch.
+// (A persistent mirror kernel's take counter and exit count sit at
+// kQueueMirror / kQueueMirrorExit, zeroed by its own last workgroup.)
 constexpr int kQueueShards = 8, kQueueNext = 256, kQueueExit = 257,
-              kQueueHead = 288;
+              kQueueMirror = 264, kQueueMirrorExit = 272, kQueueHead = 288;
 
 __host__ __device__ inline int queue_cap(int ns) {
   return (ns + kQueueShards - 1) / kQueueShards;

@@ -1202,6 +1202,66 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
       SPLIT > 1 ? (q + 1) * kPass : 1 << 30);
 }
 
+// The persistent form of the mirror kernel (A/B builds, -DIDG_GRID_PERSIST=1;
+// round 6, the review's N = 8 item): a resident grid (occupancy x CUs, at
+// most nr_subgrids) whose workgroups take subgrids 0 .. nr_subgrids-1 from a
+// take counter in the queue workspace (kQueueMirror), the next index
+// requested while the current subgrid runs, and grid each exactly as
+// kernel_gridder_mirror_mi355x does (bit for bit: the same grid_mfma on the
+// same subgrid).  The last workgroup to leave zeroes the counter and its
+// exit count (kQueueMirrorExit) for the next launch.
+template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
+__global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
+    kernel_gridder_mirror_persist_mi355x(
+        const int grid_size, int subgrid_size, float image_size,
+        float w_step_in_lambda, int nr_channels, int nr_stations,
+        const idg::UVWCoordinate<float> *__restrict__ uvw,
+        const float *__restrict__ wavenumbers,
+        const float2 *__restrict__ visibilities,
+        const float *__restrict__ spheroidal,
+        const float2 *__restrict__ aterms,
+        const idg::Metadata *__restrict__ metadata,
+        float2 *__restrict__ subgrids, int *__restrict__ queue,
+        int nr_subgrids) {
+  constexpr int NW = IDG_GRID_NW;
+  __shared__ unsigned lds[MfmaLds<2 * PT, NW>::kWords];
+  __shared__ int take;
+  const int S = S_CT > 0 ? S_CT : subgrid_size;
+  const int npix = S * S;
+  const int tid = threadIdx.x;
+  if (tid == 0) take = atomicAdd(queue + kQueueMirror, 1);
+  __syncthreads();
+  int i = __builtin_amdgcn_readfirstlane(take);
+  while (i < nr_subgrids) {
+    __syncthreads();  // every thread has read `take`
+    if (tid == 0) take = atomicAdd(queue + kQueueMirror, 1);  // lands later
+    const int s = i;
+    const SubgridSetup g = setup_subgrid(metadata, s, grid_size, S,
+                                         image_size, w_step_in_lambda);
+    float *red = reinterpret_cast<float *>(lds + MfmaLds<2 * PT, NW>::kRedOff);
+    const bool mirror =
+        __syncthreads_or(prologue_scan<NW>(g, nr_channels, uvw, visibilities,
+                                           red)) == 0 &&
+        S % 2 == 0 && g.w_offset == 0.0f;
+    if (!mirror) {
+      if (tid == 0) queue_push(queue, nr_subgrids, s, s % kQueueShards);
+    } else {
+      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
+          g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
+          visibilities, spheroidal, aterms,
+          subgrids + static_cast<size_t>(s) * 4 * npix, lds,
+          prologue_max<NW>(red), 0, 1 << 30);
+    }
+    __syncthreads();  // `take` has landed; the subgrid's LDS is consumed
+    i = __builtin_amdgcn_readfirstlane(take);
+  }
+  if (tid == 0 && atomicAdd(queue + kQueueMirrorExit, 1) ==
+                      static_cast<int>(gridDim.x) - 1) {
+    queue[kQueueMirror] = 0;
+    queue[kQueueMirrorExit] = 0;
+  }
+}
+
 template <int S_CT, int CB, int PT, bool FFT = false, int PREC = kPrecTail>
 __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES_GENERAL)
     kernel_gridder_general_mi355x(
@@ -1264,16 +1324,30 @@ struct GridderSet {
 #ifndef IDG_GRID_SPLIT64
 #define IDG_GRID_SPLIT64 1
 #endif
+// IDG_GRID_PERSIST=1 (A/B builds): the S = 32 mirror kernel in its
+// persistent form (kernel_gridder_mirror_persist_mi355x).
+#ifndef IDG_GRID_PERSIST
+#define IDG_GRID_PERSIST 0
+#endif
 constexpr int mirror_split(int S) {
   return S == 64 && IDG_GRID_SPLIT64 ? 4 : 1;
+}
+template <int S_, bool FFT_, int PREC_>
+const void *mirror_kernel() {
+  if constexpr (IDG_GRID_PERSIST && S_ == 32)
+    return reinterpret_cast<const void *>(
+        &kernel_gridder_mirror_persist_mi355x<S_, 16, IDG_GRID_PT, FFT_,
+                                              PREC_>);
+  else
+    return reinterpret_cast<const void *>(
+        &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_,
+                                      mirror_split(S_)>);
 }
 template <int S_, int PPT_, bool FFT_, int PREC_>
 GridderSet gridder_set() {
   return {reinterpret_cast<const void *>(
               &kernel_gridder_mi355x<S_, PPT_, 16, 1, IDG_GRID_PT, FFT_, PREC_>),
-          reinterpret_cast<const void *>(
-              &kernel_gridder_mirror_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_,
-                                            mirror_split(S_)>),
+          mirror_kernel<S_, FFT_, PREC_>(),
           reinterpret_cast<const void *>(
               &kernel_gridder_general_mi355x<S_, 16, IDG_GRID_PT, FFT_, PREC_>)};
 }
@@ -1373,7 +1447,9 @@ KernelChoice select_gridder(const Problem &p) {
   if (mfma && IDG_GRID_SPLIT && two_kernel_form(p.nr_subgrids)) {
     if (set.mirror)
       k.parts[0] = {set.mirror, k.block, KernelChoice::kMirror,
-                    p.subgrid_size == 64 ? mirror_split(64) : 1};
+                    p.subgrid_size == 64 ? mirror_split(64)
+                    : IDG_GRID_PERSIST && p.subgrid_size == 32 ? 0
+                                                               : 1};
     k.parts[1] = {set.general, k.block, KernelChoice::kGeneral};
     // no subgrid mirror-eligible: the combined kernel, one workgroup per
     // subgrid (2.7 % faster on a w-term batch than the queue-fed kernel)

@@ -456,7 +456,7 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
   if (err != hipSuccess) return err;
   int *queue = static_cast<int *>(lease.ptr);
   if (!lease.clean) {
-    err = hipMemsetAsync(queue, 0, (kQueueExit + 1) * sizeof(int), stream);
+    err = hipMemsetAsync(queue, 0, kQueueHead * sizeof(int), stream);
     if (err != hipSuccess) return err;
   }
   const bool run_mirror = mirror.func != nullptr && !all_general;
@@ -464,11 +464,16 @@ hipError_t launch_parts(const KernelChoice &k, int nr_subgrids, void **args13,
   void *args[16];
   for (int i = 0; i < 13; ++i) args[i] = args13[i];
   args[13] = &queue;
+  args[14] = &ns;  // (read by a persistent mirror kernel only)
+  // per_subgrid 0: a persistent mirror kernel, a resident grid
+  const int mirror_grid =
+      mirror.per_subgrid > 0
+          ? nr_subgrids * mirror.per_subgrid
+          : std::min(nr_subgrids,
+                     std::max(1, resident_workgroups(mirror.func, mirror.block)));
   if (err == hipSuccess && run_mirror)
-    err = hipLaunchKernel(mirror.func,
-                          dim3(nr_subgrids * std::max(1, mirror.per_subgrid)),
-                          dim3(mirror.block), args, 0, stream);
-  args[14] = &ns;
+    err = hipLaunchKernel(mirror.func, dim3(mirror_grid), dim3(mirror.block),
+                          args, 0, stream);
   args[15] = &all;
   if (err == hipSuccess)
     err = hipLaunchKernel(general.func, dim3(std::min(nr_subgrids, resident)),

@@ -137,7 +137,8 @@ struct KernelChoice {
     const void *func = nullptr;
     int block = 0;
     int kind = kPlain;
-    int per_subgrid = 1;  // workgroups per subgrid (mirror part: grid x)
+    int per_subgrid = 1;  // workgroups per subgrid (mirror part: grid x;
+                          // 0: a persistent mirror kernel, resident grid)
   } parts[2], all_general;
 };
 
