@@ -316,7 +316,7 @@ __device__ __forceinline__ void l2_prefetch_dma(const void *src,
 // the subgrid's own output slot (32 KB at S = 32, one pass), which only the
 // epilogue writes, after the master is read back.
 template <int S_CT, int PT, int CB, int NW, bool MIRROR, bool FFT = false,
-          int PREC = kPrecTail, bool PRESCAN = false>
+          int PREC = kPrecTail, bool PRESCAN = false, bool OPAQUE_TID = !MIRROR>
 __device__ __forceinline__ void grid_mfma(
     const SubgridSetup &g, int S, int npix, float image_size, int C,
     int nr_stations, const idg::UVWCoordinate<float> *__restrict__ uvw,
@@ -326,13 +326,13 @@ __device__ __forceinline__ void grid_mfma(
     float2 *__restrict__ out, unsigned *lds, float vmax_pre = 0.0f,
     int pass_lo = 0, int pass_hi = 1 << 30) {
   static_assert(CB % 4 == 0, "anchor blocks hold whole channel quads");
-  // General path: an opaque copy of the thread index, so values derived
-  // from it are formed per call, not hoisted out of the general kernel's
-  // loop over subgrids and kept live (spilled) across it (scratch 408 -> 160
-  // B/lane gridder, 168 -> 68 degridder at S = 32; the mirror path, one
-  // subgrid per workgroup, is better without it).
+  // General path (and the persistent mirror kernel): an opaque copy of the
+  // thread index, so values derived from it are formed per call, not hoisted
+  // out of the kernel's loop over subgrids and kept live (spilled) across it
+  // (scratch 408 -> 160 B/lane gridder, 168 -> 68 degridder at S = 32; the
+  // mirror path, one subgrid per workgroup, is better without it).
   int tid = threadIdx.x;
-  if constexpr (!MIRROR) asm volatile("" : "+v"(tid));
+  if constexpr (OPAQUE_TID) asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, col = lane & 15;
   // MIRROR: base pixels b < npix/2 (mirror npix-1-b shares the phasor);
@@ -1246,7 +1246,7 @@ __global__ void __launch_bounds__(64 * IDG_GRID_NW, IDG_GRID_WAVES)
     if (!mirror) {
       if (tid == 0) queue_push(queue, nr_subgrids, s, s % kQueueShards);
     } else {
-      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true>(
+      grid_mfma<S_CT, PT, CB, NW, true, FFT, PREC, true, true>(
           g, S, npix, image_size, nr_channels, nr_stations, uvw, wavenumbers,
           visibilities, spheroidal, aterms,
           subgrids + static_cast<size_t>(s) * 4 * npix, lds,
