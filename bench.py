@@ -126,7 +126,10 @@ def parse(argv=None):
                     help="must equal the torchrun world size (1 without it)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--min-warmup-s", type=float, default=1.0,
+    # 5 s: long enough that a sampler of GPU activity at a few-second
+    # interval sees the device busy before the timed steps (1 s: 3,292 /
+    # 3,287 Mvis/s, 5 s: 3,289 / 3,281, same box, profiles/r06/warmup/)
+    ap.add_argument("--min-warmup-s", type=float, default=5.0,
                     help="continue the untimed warm-up to at least this many "
                          "seconds of back-to-back steps (clock ramp, "
                          "DESIGN.md section 6); 0 = exactly --warmup steps")
