@@ -1350,7 +1350,7 @@ def reference_hip_for(workload_name, sec_per_step, t_grid, t_degrid):
     except Exception:
         return None
     out = {"source": "profiles/reference_hip.json "
-                     "(profiles/r01/reference_hip/SUMMARY.md)"}
+                     "(profiles/r06/reference_hip/SUMMARY.txt)"}
     for tag in ("fastest", "fastest_passing"):
         r = ref[tag]
         step = (r["gridder_ms"] + r["degridder_ms"]) / 1e3
